@@ -1,0 +1,105 @@
+"""ctypes binding of libmjgpu.so (C-ABI declared in include/mjgpu.h).
+
+There is no fallback: if the HIP library is missing or cannot be loaded, every entry
+point raises MjgError.  Build it with `python -m ffmpeg_distributed_amd.build`
+(or `__graft_entry__.build()`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MJG_LIBRARY", os.path.join(_PKG, "libmjgpu.so"))
+
+MJG_OK = 0
+MJG_E_INVALID = -1
+MJG_E_HIP = -2
+MJG_E_NOMEM = -3
+MJG_E_CAPACITY = -4
+MJG_E_STATE = -5
+
+MJG_F_TIMING = 1
+MJG_F_DEBUG_COEFS = 2
+MJG_F_SWS_NO_BITEXACT = 4
+
+KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write")
+MJG_NUM_KERNELS = len(KERNEL_NAMES)
+
+# Every symbol include/mjgpu.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_open", "mjg_close",
+    "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch",
+    "mjg_output_device", "mjg_stream", "mjg_host_alloc", "mjg_host_free",
+    "mjg_kernel_times", "mjg_debug_coefs", "mjg_debug_planes", "mjg_debug_filter",
+)
+
+
+class MjgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mjgpu error {code}: {msg}")
+        self.code = code
+
+
+class MjgConfig(C.Structure):
+    _fields_ = [
+        ("src_w", C.c_int32), ("src_h", C.c_int32),
+        ("dst_w", C.c_int32), ("dst_h", C.c_int32),
+        ("in_full_range", C.c_int32), ("qscale", C.c_int32),
+        ("sar_num", C.c_int32), ("sar_den", C.c_int32),
+        ("max_batch", C.c_int32), ("flags", C.c_uint32),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libmjgpu.so (raises MjgError if it is absent: no CPU fallback exists)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise MjgError(MJG_E_STATE, f"{LIB_PATH} not built; run python -m ffmpeg_distributed_amd.build")
+        L = C.CDLL(LIB_PATH)
+        vp, u8p, sz = C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t
+        L.mjg_version.restype = C.c_int
+        L.mjg_last_error.restype = C.c_char_p
+        L.mjg_device_count.restype = C.c_int
+        L.mjg_open.argtypes = [C.c_int, C.POINTER(MjgConfig), C.POINTER(vp)]
+        L.mjg_close.argtypes = [vp]
+        L.mjg_close.restype = None
+        L.mjg_frame_bytes.argtypes = [vp]
+        L.mjg_frame_bytes.restype = sz
+        L.mjg_header.argtypes = [vp, u8p, sz, C.POINTER(sz)]
+        L.mjg_submit.argtypes = [vp, vp, C.c_int, C.c_int]
+        L.mjg_sync.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.mjg_fetch.argtypes = [vp, vp, sz]
+        L.mjg_output_device.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+        L.mjg_stream.argtypes = [vp]
+        L.mjg_stream.restype = vp
+        L.mjg_host_alloc.argtypes = [sz, C.POINTER(vp)]
+        L.mjg_host_free.argtypes = [vp]
+        L.mjg_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_int]
+        L.mjg_debug_coefs.argtypes = [vp, C.c_int, C.POINTER(C.c_int16), sz]
+        L.mjg_debug_planes.argtypes = [vp, C.c_int, u8p, sz]
+        L.mjg_debug_filter.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int16),
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        for name in EXPORTS:  # fail loudly on a stale / partial build
+            getattr(L, name)
+        _lib = L
+        return L
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        msg = load().mjg_last_error().decode(errors="replace")
+        raise MjgError(rc, msg)
+    return rc
+
+
+def device_count() -> int:
+    return check(load().mjg_device_count())

@@ -1,0 +1,209 @@
+"""GPU MJPEG encoder: the per-segment encode that the reference's worker runs
+(`ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:`,
+ffmpeg_distributed.py:131-141), restricted to the profile
+`[-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int -huffman default -bitexact`.
+
+Host-side wrapper over libmjgpu.so; frames are packed I420 (yuv420p / yuvj420p), i.e.
+what `ffmpeg -f rawvideo -pix_fmt yuv420p` writes.  No CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import MjgConfig, MjgError, check
+
+
+def i420_frame_bytes(w: int, h: int) -> int:
+    return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
+
+
+def split_i420(frame: np.ndarray, w: int, h: int):
+    """Views (Y, U, V) of one packed I420 frame."""
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    f = np.asarray(frame, dtype=np.uint8).reshape(-1)
+    y = f[: w * h].reshape(h, w)
+    u = f[w * h: w * h + cw * ch].reshape(ch, cw)
+    v = f[w * h + cw * ch: w * h + 2 * cw * ch].reshape(ch, cw)
+    return y, u, v
+
+
+def pack_i420(y, u, v) -> np.ndarray:
+    return np.concatenate([np.asarray(p, np.uint8).reshape(-1) for p in (y, u, v)])
+
+
+class MjpegEncoder:
+    """One encoder context on one GPU (owns a HIP stream and device buffers)."""
+
+    def __init__(self, device: int, src_w: int, src_h: int, dst_w: Optional[int] = None,
+                 dst_h: Optional[int] = None, full_range: bool = False, qscale: int = 5,
+                 sar=(1, 1), max_batch: int = 16, timing: bool = False,
+                 debug_coefs: bool = False, sws_bitexact: bool = True):
+        self._L = _lib.load()
+        self.device = int(device)
+        self.src_w, self.src_h = int(src_w), int(src_h)
+        self.dst_w = int(dst_w if dst_w is not None else src_w)
+        self.dst_h = int(dst_h if dst_h is not None else src_h)
+        self.max_batch = int(max_batch)
+        flags = 0
+        if timing:
+            flags |= _lib.MJG_F_TIMING
+        if debug_coefs:
+            flags |= _lib.MJG_F_DEBUG_COEFS
+        if not sws_bitexact:
+            flags |= _lib.MJG_F_SWS_NO_BITEXACT
+        sar = sar or (0, 0)
+        cfg = MjgConfig(self.src_w, self.src_h, self.dst_w, self.dst_h, int(bool(full_range)),
+                        int(qscale), int(sar[0]), int(sar[1]), self.max_batch, flags)
+        h = C.c_void_p()
+        check(self._L.mjg_open(self.device, C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.frame_bytes = int(self._L.mjg_frame_bytes(h))
+        self._n = 0
+        self._sizes = np.zeros(self.max_batch + 1, np.uint64)
+
+    # ------------------------------------------------------------------ basics
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mjg_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return int(self._L.mjg_stream(self._h) or 0)
+
+    def header(self) -> bytes:
+        n = C.c_size_t()
+        check(self._L.mjg_header(self._h, None, 0, C.byref(n)))
+        buf = (C.c_uint8 * n.value)()
+        check(self._L.mjg_header(self._h, buf, n.value, C.byref(n)))
+        return bytes(buf)
+
+    # ------------------------------------------------------------------ encode
+    def submit(self, frames=None, nframes: Optional[int] = None, device_ptr: Optional[int] = None):
+        """Queue `nframes` packed I420 frames: a host buffer (numpy / bytes) or a device
+        pointer (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU)."""
+        if device_ptr is not None:
+            if nframes is None:
+                raise ValueError("nframes is required with device_ptr")
+            check(self._L.mjg_submit(self._h, C.c_void_p(int(device_ptr)), int(nframes), 1))
+            self._n = int(nframes)
+            return
+        arr = np.ascontiguousarray(np.frombuffer(frames, dtype=np.uint8)
+                                   if isinstance(frames, (bytes, bytearray, memoryview))
+                                   else np.asarray(frames, dtype=np.uint8))
+        if arr.size % self.frame_bytes:
+            raise ValueError(f"buffer of {arr.size} bytes is not a whole number of "
+                             f"{self.frame_bytes}-byte I420 frames")
+        n = arr.size // self.frame_bytes if nframes is None else int(nframes)
+        self._keep = arr  # the async H2D copy reads it until sync()
+        check(self._L.mjg_submit(self._h, C.c_void_p(arr.ctypes.data), n, 0))
+        self._n = n
+
+    def sync(self) -> np.ndarray:
+        total = C.c_uint64()
+        check(self._L.mjg_sync(self._h, self._sizes.ctypes.data_as(C.POINTER(C.c_uint64)),
+                               C.byref(total)))
+        self._keep = None
+        return self._sizes[: self._n].copy()
+
+    def fetch(self) -> List[bytes]:
+        sizes = self.sync()
+        total = int(sizes.sum())
+        buf = np.empty(max(total, 1), np.uint8)
+        check(self._L.mjg_fetch(self._h, C.c_void_p(buf.ctypes.data), buf.size))
+        out, o = [], 0
+        for s in sizes:
+            out.append(buf[o: o + int(s)].tobytes())
+            o += int(s)
+        return out
+
+    def encode(self, frames) -> List[bytes]:
+        """Encode host frames (any count; split into max_batch submits)."""
+        arr = np.ascontiguousarray(np.asarray(frames, dtype=np.uint8)).reshape(-1)
+        n = arr.size // self.frame_bytes
+        out: List[bytes] = []
+        for i in range(0, n, self.max_batch):
+            k = min(self.max_batch, n - i)
+            self.submit(arr[i * self.frame_bytes:(i + k) * self.frame_bytes], k)
+            out.extend(self.fetch())
+        return out
+
+    def output_device(self):
+        data, offs = C.c_void_p(), C.c_void_p()
+        check(self._L.mjg_output_device(self._h, C.byref(data), C.byref(offs)))
+        return int(data.value or 0), int(offs.value or 0)
+
+    # ------------------------------------------------------------------ timing/debug
+    def kernel_times(self, reset: bool = False):
+        ms = (C.c_double * _lib.MJG_NUM_KERNELS)()
+        n = C.c_int()
+        check(self._L.mjg_kernel_times(self._h, ms, C.byref(n), int(bool(reset))))
+        return {k: ms[i] for i, k in enumerate(_lib.KERNEL_NAMES)}, n.value
+
+    def debug_coefs(self, frame: int = 0) -> np.ndarray:
+        nmcu = ((self.dst_w + 15) // 16) * ((self.dst_h + 15) // 16)
+        out = np.zeros((nmcu * 6, 64), np.int16)
+        check(self._L.mjg_debug_coefs(self._h, int(frame), out.ctypes.data_as(C.POINTER(C.c_int16)),
+                                      out.shape[0]))
+        return out
+
+    def debug_planes(self, frame: int = 0) -> np.ndarray:
+        n = i420_frame_bytes(self.dst_w, self.dst_h)
+        out = np.zeros(n, np.uint8)
+        check(self._L.mjg_debug_planes(self._h, int(frame), out.ctypes.data_as(C.POINTER(C.c_uint8)), n))
+        return out
+
+    def debug_filter(self, plane: int, direction: int):
+        taps, ln = C.c_int(), C.c_int()
+        check(self._L.mjg_debug_filter(self._h, plane, direction, None, None, C.byref(taps),
+                                       C.byref(ln)))
+        coeff = np.zeros((ln.value, taps.value), np.int16)
+        pos = np.zeros(ln.value, np.int32)
+        check(self._L.mjg_debug_filter(self._h, plane, direction,
+                                       coeff.ctypes.data_as(C.POINTER(C.c_int16)),
+                                       pos.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       C.byref(taps), C.byref(ln)))
+        return coeff, pos
+
+
+class PinnedBuffer:
+    """Page-locked host buffer from mjg_host_alloc (fast async H2D for submits)."""
+
+    def __init__(self, nbytes: int):
+        self._L = _lib.load()
+        p = C.c_void_p()
+        check(self._L.mjg_host_alloc(int(nbytes), C.byref(p)))
+        self.ptr = int(p.value)
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            self._L.mjg_host_free(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+__all__ = ["MjpegEncoder", "MjgError", "PinnedBuffer", "i420_frame_bytes", "split_i420",
+           "pack_i420"]

@@ -1,0 +1,125 @@
+/*
+ * mjgpu.h -- C-ABI of libmjgpu.so, the MI355X (gfx950) MJPEG segment encoder.
+ *
+ * Drop-in boundary.  The reference (Rouji/ffmpeg_distributed) has no FFI: its hot
+ * path is the per-segment worker process built at ffmpeg_distributed.py:131-138
+ *     nice -n10 ionice -c3 ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:
+ * and launched/supervised at ffmpeg_distributed.py:139-141 (FFMPEGProc.run,
+ * ffmpeg_distributed.py:59-91).  For the north-star profile
+ *     [-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int -huffman default -bitexact
+ * this library replaces the arithmetic that worker runs (swscale bicubic + tv->pc
+ * range conversion, jfdctint + quantiser + default-table Huffman + 0xFF stuffing)
+ * and the Python host code in ffmpeg_distributed_amd/ (worker.py, dispatcher.py)
+ * replaces the process around it with the same stdin/stdout/stderr/exit-code
+ * contract.  Plain C types only; no torch types cross this boundary.
+ *
+ * Threading: one mjg_ctx per (device, caller thread); a ctx owns its HIP stream,
+ * device buffers and filter tables.  Calls on different contexts may run
+ * concurrently.  The library never writes to stdout (stdout is the data stream).
+ * Every call returns MJG_OK (0) or a negative MJG_E_* code; mjg_last_error()
+ * returns a thread-local description of the last failure.
+ */
+#ifndef MJGPU_H
+#define MJGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MJG_OK 0
+#define MJG_E_INVALID (-1)     /* bad argument / unsupported geometry */
+#define MJG_E_HIP (-2)         /* HIP runtime error (no device, launch failure ...) */
+#define MJG_E_NOMEM (-3)       /* device or pinned-host allocation failed */
+#define MJG_E_CAPACITY (-4)    /* caller buffer too small */
+#define MJG_E_STATE (-5)       /* call out of order (e.g. fetch before submit) */
+
+/* mjg_config.flags */
+#define MJG_F_TIMING 1u        /* record HIP events around every kernel launch */
+#define MJG_F_DEBUG_COEFS 2u   /* keep quantized coefficients of every block (tests) */
+#define MJG_F_SWS_NO_BITEXACT 4u /* swscale filter tables without SWS_BITEXACT */
+
+/* Kernel ids for mjg_kernel_times() */
+#define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane)        */
+#define MJG_K_ENCODE 1         /* load + FDCT + quant + Huffman -> per-chunk bits     */
+#define MJG_K_SCAN_BITS 2      /* per-frame exclusive scan of chunk bit lengths      */
+#define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk      */
+#define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes        */
+#define MJG_K_WRITE 5          /* header + stuffed scan + EOI into packed output     */
+#define MJG_NUM_KERNELS 6
+
+typedef struct mjg_config {
+  int32_t src_w, src_h;      /* decoded frame size (packed I420: Y, then U, then V)    */
+  int32_t dst_w, dst_h;      /* encoded size; == src when remote_args has no -vf scale */
+  int32_t in_full_range;     /* 1: yuvj420p input; 0: yuv420p (tv) -> tv->pc as swscale */
+  int32_t qscale;            /* effective mpegvideo qscale, 2..31 (see -q:v mapping)   */
+  int32_t sar_num, sar_den;  /* JFIF APP0 density; 0/0 omits APP0 (unknown SAR)        */
+  int32_t max_batch;         /* most frames one mjg_submit() may carry                 */
+  uint32_t flags;            /* MJG_F_*                                                */
+} mjg_config;
+
+typedef struct mjg_ctx mjg_ctx;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int mjg_version(void);
+/* Thread-local text of the last error (never NULL). */
+const char *mjg_last_error(void);
+/* Number of visible HIP devices, or a negative MJG_E_* code. */
+int mjg_device_count(void);
+
+/* Create a context on `device`: validates cfg, builds quant/Huffman/filter tables,
+ * allocates device buffers for cfg->max_batch frames.  Replaces one
+ * `ffmpeg ... <remote_args>` worker's codec/scaler initialisation
+ * (ffmpeg_distributed.py:131-138). */
+int mjg_open(int device, const mjg_config *cfg, mjg_ctx **out);
+void mjg_close(mjg_ctx *ctx);
+
+/* Bytes of one packed I420 input frame (src_w x src_h). */
+size_t mjg_frame_bytes(const mjg_ctx *ctx);
+/* The constant per-config JPEG header (SOI .. SOS) every frame starts with. */
+int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
+
+/* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously on the ctx
+ * stream.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
+ * staging buffer; pinned memory from mjg_host_alloc() makes this asynchronous);
+ * src_is_device = 1: `frames` is device memory on ctx's device, read in place.
+ * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
+int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
+/* Wait for the last submit.  frame_sizes (may be NULL) receives nframes JPEG sizes;
+ * *total (may be NULL) the packed total.  Grows the output buffer and re-runs the
+ * final kernel if the packed output exceeded its capacity. */
+int mjg_sync(mjg_ctx *ctx, uint64_t *frame_sizes, uint64_t *total);
+/* Copy the packed JPEGs of the last submit (frame after frame) to host memory. */
+int mjg_fetch(mjg_ctx *ctx, uint8_t *out, size_t cap);
+/* Device pointers of the packed output and of the per-frame byte offsets (nframes+1
+ * entries, valid after mjg_sync). */
+int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offsets);
+/* The hipStream_t the context launches on (for event timing by the caller). */
+void *mjg_stream(mjg_ctx *ctx);
+
+/* Pinned host memory for mjg_submit / mjg_fetch. */
+int mjg_host_alloc(size_t bytes, void **ptr);
+int mjg_host_free(void *ptr);
+
+/* Average device time (ms) per launch of each kernel (MJG_K_*) since the last reset,
+ * and the number of submits it was averaged over.  Needs MJG_F_TIMING. */
+int mjg_kernel_times(mjg_ctx *ctx, double *ms /* [MJG_NUM_KERNELS] */, int *launches, int reset);
+
+/* Test hooks (tests/ only). */
+/* Quantized coefficients (natural order) of frame `frame` of the last submit, blocks
+ * in MCU order (Y0 Y1 Y2 Y3 Cb Cr per MCU).  Needs MJG_F_DEBUG_COEFS. */
+int mjg_debug_coefs(mjg_ctx *ctx, int frame, int16_t *out, size_t nblocks);
+/* The full-range encoder-input planes (after scale/range stage) of frame `frame`,
+ * packed I420 at dst size.  Only meaningful when the config scales. */
+int mjg_debug_planes(mjg_ctx *ctx, int frame, uint8_t *out, size_t cap);
+/* Filter tables the context generated: plane 0 = luma, 1 = chroma; dir 0 = horizontal,
+ * 1 = vertical.  taps/len may be queried with coeff == NULL. */
+int mjg_debug_filter(mjg_ctx *ctx, int plane, int dir, int16_t *coeff, int32_t *pos,
+                     int *taps, int *len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJGPU_H */

@@ -1,0 +1,191 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle, byte for byte.
+
+The oracle restates FFmpeg's mjpeg encoder / swscale (oracle/mjpeg_oracle.c); parity
+against FFmpeg itself is unpinned (FFmpeg is absent on this pool).
+"""
+import io
+
+import numpy as np
+import pytest
+
+import oracle
+from ffmpeg_distributed_amd.encoder import MjpegEncoder, split_i420, pack_i420, i420_frame_bytes
+from ffmpeg_distributed_amd.testsrc import testsrc2_i420 as make_testsrc
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_frames(w, h, n, seed, kind="noise"):
+    rng = np.random.default_rng(seed)
+    fb = i420_frame_bytes(w, h)
+    if kind == "noise":
+        return rng.integers(0, 256, (n, fb), dtype=np.uint8)
+    if kind == "smooth":
+        out = []
+        for i in range(n):
+            yy, xx = np.mgrid[0:h, 0:w]
+            cw, ch = (w + 1) // 2, (h + 1) // 2
+            cy, cx = np.mgrid[0:ch, 0:cw]
+            y = (128 + 90 * np.sin(xx / (5 + i) + yy / 9) + rng.normal(0, 3, (h, w))).clip(0, 255)
+            u = (128 + 50 * np.cos(cx / 4 + i)).clip(0, 255) + 0 * cy
+            v = (128 + 50 * np.sin(cy / 3 - i)).clip(0, 255) + 0 * cx
+            out.append(pack_i420(y.astype(np.uint8), u.astype(np.uint8), v.astype(np.uint8)))
+        return np.stack(out)
+    if kind == "flat":
+        return np.full((n, fb), 255 if seed % 2 else 0, np.uint8)
+    if kind == "checker":
+        out = []
+        for i in range(n):
+            yy, xx = np.mgrid[0:h, 0:w]
+            y = np.where(((xx + yy + i) & 1) == 0, 255, 0).astype(np.uint8)
+            cw, ch = (w + 1) // 2, (h + 1) // 2
+            cy, cx = np.mgrid[0:ch, 0:cw]
+            u = np.where(((cx // 2 + cy // 2) & 1) == 0, 255, 0).astype(np.uint8)
+            v = (255 - u).astype(np.uint8)
+            out.append(pack_i420(y, u, v))
+        return np.stack(out)
+    if kind == "testsrc":
+        return np.stack([make_testsrc(w, h, seed + i) for i in range(n)])
+    raise ValueError(kind)
+
+
+def oracle_frames(frames, w, h, q, full_range, dw=None, dh=None, sar=(1, 1)):
+    out = []
+    for f in frames:
+        y, u, v = split_i420(f, w, h)
+        out.append(oracle.encode_frame(y, u, v, dst_w=dw, dst_h=dh, full_range=full_range,
+                                       qscale=q, sar=sar))
+    return out
+
+
+def first_diff(a: bytes, b: bytes):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i] != b[i]:
+            return i
+    return n if len(a) != len(b) else -1
+
+
+CASES = [
+    # (w, h, q, full_range, kind)
+    (72, 40, 5, False, "smooth"),
+    (64, 48, 5, True, "smooth"),
+    (72, 40, 2, False, "noise"),
+    (72, 40, 31, True, "noise"),
+    (16, 16, 5, True, "flat"),
+    (8, 8, 3, False, "smooth"),
+    (130, 66, 4, False, "checker"),
+    (101, 57, 7, True, "smooth"),
+    (1920, 1080, 5, False, "testsrc"),
+    (1280, 720, 2, True, "noise"),
+]
+
+
+@pytest.mark.parametrize("w,h,q,full,kind", CASES)
+def test_encode_matches_oracle(w, h, q, full, kind):
+    n = 3
+    frames = rand_frames(w, h, n, seed=w * 31 + h + q, kind=kind)
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=4) as enc:
+        got = enc.encode(frames)
+    ref = oracle_frames(frames, w, h, q, full)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+@pytest.mark.parametrize("w,h,q,full", [(72, 40, 5, False), (1920, 1080, 3, True)])
+def test_coefficients_match_oracle(w, h, q, full):
+    frames = rand_frames(w, h, 2, seed=1, kind="smooth" if w < 200 else "testsrc")
+    with MjpegEncoder(0, w, h, qscale=q, full_range=True, max_batch=2, debug_coefs=True) as enc:
+        enc.submit(frames)
+        enc.sync()
+        for i in range(2):
+            y, u, v = split_i420(frames[i], w, h)
+            ref, _ = oracle.frame_coeffs(y, u, v, q)
+            got = enc.debug_coefs(i)
+            bad = np.nonzero((got != ref).any(1))[0]
+            assert bad.size == 0, (i, bad[:10])
+
+
+def test_batching_and_reuse():
+    w, h, q = 96, 64, 6
+    frames = rand_frames(w, h, 7, seed=3, kind="smooth")
+    ref = oracle_frames(frames, w, h, q, False)
+    with MjpegEncoder(0, w, h, qscale=q, max_batch=3) as enc:
+        got = enc.encode(frames)          # 3 + 3 + 1 frames
+        got2 = enc.encode(frames[::-1])   # context reuse, different order
+    assert got == ref
+    assert got2 == ref[::-1]
+
+
+def test_sar_and_header():
+    w, h = 48, 32
+    frames = rand_frames(w, h, 1, seed=9, kind="smooth")
+    for sar in [(1, 1), (0, 0), (4, 3)]:
+        with MjpegEncoder(0, w, h, qscale=5, sar=sar, max_batch=1) as enc:
+            got = enc.encode(frames)[0]
+            hdr = enc.header()
+        ref = oracle_frames(frames, w, h, 5, False, sar=sar)[0]
+        assert got == ref
+        assert got.startswith(hdr)
+        assert hdr == oracle.header(w, h, 5, sar=sar)
+
+
+def test_output_overflow_regrow():
+    # noise at q=2 compresses worse than raw: exercises the grow-and-rewrite path
+    w, h = 256, 128
+    frames = rand_frames(w, h, 4, seed=5, kind="noise")
+    with MjpegEncoder(0, w, h, qscale=2, full_range=True, max_batch=4) as enc:
+        got = enc.encode(frames)
+    assert got == oracle_frames(frames, w, h, 2, True)
+
+
+@pytest.mark.parametrize("sw,sh,dw,dh,full", [
+    (3840, 2160, 1920, 1080, False),
+    (160, 96, 80, 48, False),
+    (160, 96, 80, 48, True),
+    (100, 60, 64, 40, False),
+    (64, 48, 100, 70, True),
+])
+def test_scale_matches_oracle(sw, sh, dw, dh, full):
+    n = 2
+    kind = "testsrc" if sw >= 1000 else "smooth"
+    frames = rand_frames(sw, sh, n, seed=11, kind=kind)
+    q = 3
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2) as enc:
+        enc.submit(frames)
+        enc.sync()
+        planes = [enc.debug_planes(i) for i in range(n)]
+        for p in range(2):
+            for d in range(2):
+                coeff, pos = enc.debug_filter(p, d)
+                src = (sw if p == 0 else (sw + 1) // 2) if d == 0 else (sh if p == 0 else (sh + 1) // 2)
+                dst = (dw if p == 0 else (dw + 1) // 2) if d == 0 else (dh if p == 0 else (dh + 1) // 2)
+                rc, rp = oracle.sws_filter(src, dst, 1 << (14 if d == 0 else 12), 4 if d == 0 else 2,
+                                           src_pos=128, dst_pos=128)
+                assert (coeff == rc).all() and (pos == rp).all(), (p, d)
+        got = enc.fetch()
+    for i in range(n):
+        y, u, v = split_i420(frames[i], sw, sh)
+        ry = oracle.scale_plane(y, dw, dh, 0 if full else 1)
+        ru = oracle.scale_plane(u, (dw + 1) // 2, (dh + 1) // 2, 0 if full else 2, chroma=True)
+        rv = oracle.scale_plane(v, (dw + 1) // 2, (dh + 1) // 2, 0 if full else 2, chroma=True)
+        gy, gu, gv = split_i420(planes[i], dw, dh)
+        assert (gy == ry).all() and (gu == ru).all() and (gv == rv).all()
+    assert got == oracle_frames(frames, sw, sh, q, full, dw, dh)
+
+
+def test_4k_full_size_properties():
+    """BASELINE config 2 size: decodable, deterministic, equal to the oracle on frame 0."""
+    from PIL import Image
+    w, h = 3840, 2160
+    frames = np.stack([make_testsrc(w, h, t) for t in range(4)])
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=4) as enc:
+        a = enc.encode(frames)
+        b = enc.encode(frames)
+    assert a == b
+    for j in a:
+        im = Image.open(io.BytesIO(j))
+        im.load()
+        assert im.size == (w, h)
+    y, u, v = split_i420(frames[0], w, h)
+    assert a[0] == oracle.encode_frame(y, u, v, qscale=5)
