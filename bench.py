@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path named by BASELINE.json: 4K yuv420p MJPEG q=5 segment encode
+(configs[1]: "4K60 60 s testsrc2 yuv420p MJPEG q=5 on one MI355X").
+
+A step = one 2-second segment (120 frames of 3840x2160 yuv420p) encoded on one GPU,
+frames already resident in HBM (a pool of distinct synthetic testsrc2-like frames
+generated on the device), JPEG output packed in HBM.  Default K=30 steps = the 60 s
+(3600-frame) clip of configs[1].  Multi-GPU: one process per GPU
+(torch.distributed.run), segments sharded with no data-path collective (weak scaling);
+the barrier / max-over-ranks timing uses the process group only for bookkeeping.
+
+Prints ONE JSON line on rank 0 (see the driver contract in the task description).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+W, H, Q, SEG = 3840, 2160, 5, 120
+METRIC = "encoded frames/sec (node), 4K yuv420p MJPEG q=5 at 1/2/4/8 GPUs; HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--pool", type=int, default=480, help="distinct resident frames per GPU")
+    p.add_argument("--seg", type=int, default=SEG)
+    p.add_argument("--cpu-sample-frames", type=int, default=96)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_encode_4k_q5.json"),
+                   help="PMC traffic summary written by tools/pmc_traffic.py")
+    return p.parse_args()
+
+
+def cpu_baseline(nframes: int):
+    """Oracle ('port') on the host cores: bounded sample of the same workload."""
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores, initializer=_cpu_init) as pool:
+        pool.map(_cpu_warm, range(cores))
+        t0 = time.perf_counter()
+        sizes = pool.map(_cpu_encode, range(nframes))
+        dt = time.perf_counter() - t0
+    return {"value": nframes / dt, "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{nframes} frames 3840x2160 yuv420p q=5 (testsrc2-like, 8 distinct), "
+                      f"oracle/mjpeg_oracle.c (C restatement of FFmpeg's mjpeg+swscale path), "
+                      f"{cores} processes, {dt:.1f} s wall",
+            "mean_jpeg_bytes": float(sum(sizes) / len(sizes))}
+
+
+_CPU_FRAMES = None
+
+
+def _cpu_init():
+    global _CPU_FRAMES
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420
+    from ffmpeg_distributed_amd.encoder import split_i420
+    _CPU_FRAMES = [split_i420(testsrc2_i420(W, H, t), W, H) for t in range(0, 8)]
+
+
+def _cpu_warm(_):
+    import oracle
+    oracle.lib()
+    return 0
+
+
+def _cpu_encode(i):
+    import oracle
+    y, u, v = _CPU_FRAMES[i % len(_CPU_FRAMES)]
+    return len(oracle.encode_frame(y, u, v, qscale=Q))
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+
+    import torch
+    import torch.distributed as dist
+    from ffmpeg_distributed_amd import build as B
+    B.build()
+    from ffmpeg_distributed_amd.encoder import MjpegEncoder
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # resident input pool: distinct frames, different per rank (rank's own segments)
+    seg = a.seg
+    pool_n = max(seg, (a.pool // seg) * seg)
+    fb = W * H * 3 // 2
+    pool = torch.empty((pool_n, fb), dtype=torch.uint8, device=dev)
+    gen = 20
+    for i in range(0, pool_n, gen):
+        k = min(gen, pool_n - i)
+        pool[i:i + k] = testsrc2_i420_torch(W, H, rank * 100000 + i, k, dev)
+    torch.cuda.synchronize()
+
+    enc = MjpegEncoder(local, W, H, qscale=Q, max_batch=seg, timing=True)
+    nseg_pool = pool_n // seg
+    bytes_out = []
+
+    def step(s):
+        base = pool[(s % nseg_pool) * seg]
+        enc.submit(device_ptr=base.data_ptr(), nframes=seg)
+        sizes = enc.sync()
+        bytes_out.append(int(sizes.sum()))
+
+    for s in range(a.warmup):
+        step(s)
+    enc.kernel_times(reset=True)
+    bytes_out.clear()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        step(a.warmup + s)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    kt, nl = enc.kernel_times()
+
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    frames_total = a.steps * seg * world
+    value = frames_total / dt
+    mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
+
+    # Roofline of the dominant kernel (k_encode): algorithmic bytes per launch =
+    # (input planes 12,441,600 B + JPEG bytes written) x frames per launch.
+    enc_ms = kt["encode"]
+    alg_bytes = (fb + mean_jpeg) * seg
+    achieved = alg_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms > 0 else 0.0
+    traffic = None
+    try:
+        with open(a.pmc) as f:
+            pm = json.load(f)
+        if pm.get("workload", {}).get("frames_per_launch") == seg:
+            traffic = pm.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(a.cpu_sample_frames)
+            except Exception as e:  # reported, never fatal for the GPU number
+                cpu = {"value": None, "error": repr(e)}
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: testsrc2-like generator, frames resident in HBM "
+                    f"({pool_n} distinct per GPU), output packed in HBM",
+            "config": {"workload": "4K60 testsrc2 yuv420p MJPEG q=5 (BASELINE configs[1]); "
+                                   "step = one 2 s segment", "width": W, "height": H,
+                       "qscale": Q, "frames_per_step": seg, "global_batch": seg * world,
+                       "parallelism": f"segment-dp{world}",
+                       "profile": "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact"},
+            "roofline": {"bound": "hbm", "kernel": "k_encode",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "alg_bytes_per_launch": int(alg_bytes),
+                         "avg_launch_ms": round(enc_ms, 4), "launches": nl},
+            "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},
+            "mean_jpeg_bytes": round(mean_jpeg, 1),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    enc.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -32,7 +32,8 @@ EXPORTS = (
     "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_open", "mjg_close",
     "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch",
     "mjg_output_device", "mjg_stream", "mjg_host_alloc", "mjg_host_free",
-    "mjg_kernel_times", "mjg_debug_coefs", "mjg_debug_planes", "mjg_debug_filter",
+    "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
+    "mjg_debug_planes", "mjg_debug_filter",
 )
 
 
@@ -88,6 +89,9 @@ def load():
         L.mjg_debug_planes.argtypes = [vp, C.c_int, u8p, sz]
         L.mjg_debug_filter.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int16),
                                        C.POINTER(C.c_int32), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.mjg_build_header.argtypes = [C.POINTER(MjgConfig), u8p, sz, C.POINTER(sz)]
+        L.mjg_sws_filter.argtypes = [C.c_int] * 7 + [C.POINTER(C.c_int16), sz, C.POINTER(C.c_int32),
+                                                     C.POINTER(C.c_int)]
         for name in EXPORTS:  # fail loudly on a stale / partial build
             getattr(L, name)
         _lib = L
@@ -103,3 +107,29 @@ def check(rc: int) -> int:
 
 def device_count() -> int:
     return check(load().mjg_device_count())
+
+
+def build_header(dst_w: int, dst_h: int, qscale: int, sar=(1, 1)) -> bytes:
+    """The per-config JPEG header, computed on the host (no GPU needed)."""
+    L = load()
+    cfg = MjgConfig(dst_w, dst_h, dst_w, dst_h, 1, qscale, sar[0], sar[1], 1, 0)
+    n = C.c_size_t()
+    check(L.mjg_build_header(C.byref(cfg), None, 0, C.byref(n)))
+    buf = (C.c_uint8 * n.value)()
+    check(L.mjg_build_header(C.byref(cfg), buf, n.value, C.byref(n)))
+    return bytes(buf)
+
+
+def sws_filter(src_len, dst_len, one, align, bitexact=True, src_pos=128, dst_pos=128):
+    """swscale bicubic filter table as the library generates it (host side)."""
+    import numpy as np
+    L = load()
+    taps = C.c_int()
+    check(L.mjg_sws_filter(src_len, dst_len, one, align, int(bitexact), src_pos, dst_pos, None, 0,
+                           None, C.byref(taps)))
+    coeff = np.zeros(dst_len * taps.value, np.int16)
+    pos = np.zeros(dst_len, np.int32)
+    check(L.mjg_sws_filter(src_len, dst_len, one, align, int(bitexact), src_pos, dst_pos,
+                           coeff.ctypes.data_as(C.POINTER(C.c_int16)), coeff.size,
+                           pos.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(taps)))
+    return coeff.reshape(dst_len, taps.value), pos

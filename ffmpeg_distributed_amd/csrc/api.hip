@@ -1,6 +1,7 @@
 // C-ABI of libmjgpu.so (declarations and boundary citations: include/mjgpu.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -128,7 +129,8 @@ struct mjg_ctx {
   mjg_config cfg{};
   hipStream_t stream = nullptr;
   EncGeom geom{};
-  QuantTab qt{};
+  int32_t qmat[64];
+  int enc_grid = 0;
   bool scale = false;
   size_t in_frame_bytes = 0, enc_frame_bytes = 0;
   std::vector<uint8_t> hdr;
@@ -270,11 +272,13 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     int v = i == 0 ? 8 : ((kMpeg1Intra[i] * k.qscale) >> 3);
     v = v > 255 ? 255 : v;
     c->mprime[i] = (uint8_t)v;
-    c->qt.qmat[i] = (int32_t)((2ull << 21) / (uint64_t)(16 * v));
+    c->qmat[i] = (int32_t)((2ull << 21) / (uint64_t)(16 * v));
   }
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den);
 
-  uint32_t tabs[544] = {0};
+  // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
+  // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row])
+  uint32_t tabs[608] = {0};
   build_huffman(tabs, kBitsAcLum, kValAcLum);
   build_huffman(tabs + 256, kBitsAcChr, kValAcChr);
   uint32_t dc[256];
@@ -282,11 +286,11 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   for (int i = 0; i < 16; i++) tabs[512 + i] = dc[i];
   build_huffman(dc, kBitsDcChr, kValDc);
   for (int i = 0; i < 16; i++) tabs[528 + i] = dc[i];
+  for (int i = 0; i < 64; i++) tabs[544 + (i & 7) * 8 + (i >> 3)] = (uint32_t)c->qmat[i];  // [col][row]
 
   const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks;
   int rc;
-  if ((rc = dmalloc(&c->d_tabs, 544)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
-      (rc = dmalloc(&c->d_stage, B * c->in_frame_bytes)) ||
+  if ((rc = dmalloc(&c->d_tabs, 608)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
       (rc = dmalloc(&c->d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
       (rc = dmalloc(&c->d_chunk_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
@@ -320,6 +324,12 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       sg.range = k.in_full_range ? 0 : (p ? 2 : 1);
     }
   }
+
+  // persistent k_encode grid: every CU filled with as many workgroups as fit
+  int ncu = 0, per_cu = 0;
+  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode, kEncThreads, 0));
+  c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
 
   c->timing = (k.flags & MJG_F_TIMING) != 0;
   if (c->timing)
@@ -401,6 +411,10 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   const EncGeom &g = c->geom;
   const uint8_t *src = frames;
   if (!src_is_device) {
+    if (!c->d_stage) {  // staging for host submits, allocated on first use
+      const int rc = dmalloc(&c->d_stage, (size_t)c->cfg.max_batch * c->in_frame_bytes);
+      if (rc) return rc;
+    }
     HIP_TRY(hipMemcpyAsync(c->d_stage, frames, (size_t)n * c->in_frame_bytes, hipMemcpyHostToDevice,
                            c->stream));
     src = c->d_stage;
@@ -428,8 +442,9 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     enc_in = c->d_scaled;
   }
   tmark(c, MJG_K_ENCODE, 0);
-  k_encode<<<dim3(g.nchunks, n), kEncThreads, 0, c->stream>>>(enc_in, g, c->qt, c->d_tabs,
-                                                              c->d_scratch, c->d_chunk_bits, c->d_dbg);
+  const int ntasks = g.nchunks * n;
+  k_encode<<<std::min(ntasks, c->enc_grid), kEncThreads, 0, c->stream>>>(
+      enc_in, g, c->d_tabs, c->d_scratch, c->d_chunk_bits, c->d_dbg, ntasks);
   tmark(c, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_BITS, 0);
@@ -538,6 +553,37 @@ int mjg_kernel_times(mjg_ctx *c, double *ms, int *launches, int reset) {
   return MJG_OK;
 }
 
+int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *len) {
+  if (!cfg) return set_err(MJG_E_INVALID, "null cfg");
+  if (cfg->dst_w < 1 || cfg->dst_h < 1 || cfg->dst_w > 65535 || cfg->dst_h > 65535 ||
+      cfg->qscale < 1 || cfg->qscale > 31)
+    return set_err(MJG_E_INVALID, "bad size / qscale");
+  uint8_t mp[64];
+  for (int i = 0; i < 64; i++) {
+    const int v = i == 0 ? 8 : ((kMpeg1Intra[i] * cfg->qscale) >> 3);
+    mp[i] = (uint8_t)(v > 255 ? 255 : v);
+  }
+  const std::vector<uint8_t> h = build_header(cfg->dst_w, cfg->dst_h, mp, cfg->sar_num, cfg->sar_den);
+  if (len) *len = h.size();
+  if (!out) return MJG_OK;
+  if (cap < h.size()) return set_err(MJG_E_CAPACITY, "header needs %zu bytes", h.size());
+  memcpy(out, h.data(), h.size());
+  return MJG_OK;
+}
+
+int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, int src_pos,
+                   int dst_pos, int16_t *coeff, size_t coeff_cap, int32_t *pos_out, int *taps) {
+  SwsFilter f;
+  if (!make_sws_filter(src_len, dst_len, one, align, bitexact != 0, src_pos, dst_pos, &f))
+    return set_err(MJG_E_INVALID, "unsupported filter %d -> %d", src_len, dst_len);
+  if (taps) *taps = f.taps;
+  if (!coeff) return MJG_OK;
+  if (coeff_cap < f.coeff.size()) return set_err(MJG_E_CAPACITY, "need %zu taps", f.coeff.size());
+  memcpy(coeff, f.coeff.data(), f.coeff.size() * sizeof(int16_t));
+  if (pos_out) memcpy(pos_out, f.pos.data(), f.pos.size() * sizeof(int32_t));
+  return MJG_OK;
+}
+
 int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
   if (!c->d_dbg) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
@@ -546,8 +592,11 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   const size_t nb = (size_t)c->geom.nmcu * 6;
   if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
-  HIP_TRY(hipMemcpy(out, c->d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
+  std::vector<int16_t> zz(nb * 64);  // kernel stores zigzag order
+  HIP_TRY(hipMemcpy(zz.data(), c->d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
                     hipMemcpyDeviceToHost));
+  for (size_t b = 0; b < nb; b++)
+    for (int k = 0; k < 64; k++) out[b * 64 + kZigzag[k]] = zz[b * 64 + k];
   return MJG_OK;
 }
 

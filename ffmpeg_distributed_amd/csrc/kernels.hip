@@ -21,11 +21,15 @@
 
 #include "jpeg_tables.h"
 
+#ifndef MJG_ABLATE
+#define MJG_ABLATE 0  // perf experiments only: 1 = no bit-pack
+#endif
+
 namespace mjg {
 
 constexpr int kMcuPerChunk = 64;
 constexpr int kEncThreads = 6 * 64;  // 6 blocks per MCU x 64 MCUs, one block per thread
-constexpr int kWinWords = 4096;      // LDS bit-pack window (16 KiB)
+constexpr int kWinWords = 2048;      // LDS bit-pack window (8 KiB)
 constexpr int kMaxBlockBits = 1664;  // >= DC 16 + 63 * (16 + 10) bits
 constexpr int kSlotWords = (kMcuPerChunk * 6 * kMaxBlockBits + 31) / 32;
 
@@ -39,23 +43,19 @@ struct EncGeom {
   int debug_coefs;
 };
 
-struct QuantTab {
-  int32_t qmat[64];  // natural order, floor(2^18 / m'[i])
-};
 
 // ---------------------------------------------------------------- helpers
+// swscale's unscaled yuv420p -> yuvj420p path per sample: hScale8To15 (1 tap, 1<<14)
+// -> lumRangeToJpeg_c / chrRangeToJpeg_c -> yuv2plane1_8_c (flat 64 dither), i.e.
+//   Y: clip_u8((((min(p<<7, 30189) * 19077 - 39057361) >> 14) + 64) >> 7)
+//   C: clip_u8((((min(p<<7, 30775) *  4663 -  9289992) >> 12) + 64) >> 7)
+// The nested floors fold to one shift and the input clamps are subsumed by the output
+// clamp (checked exhaustively for p = 0..255 in tests/test_oracle.py).
 __device__ __forceinline__ int range_luma(int p) {
-  // hScale8To15 (1 tap, 1<<14) -> lumRangeToJpeg_c -> yuv2plane1_8_c (flat 64 dither)
-  int v = min(p << 7, 30189);
-  v = (v * 19077 - 39057361) >> 14;
-  v = (v + 64) >> 7;
-  return min(max(v, 0), 255);
+  return min(max((__mul24(p, 2441856) - 38008785) >> 21, 0), 255);
 }
 __device__ __forceinline__ int range_chroma(int p) {
-  int v = min(p << 7, 30775);
-  v = (v * 4663 - 9289992) >> 12;
-  v = (v + 64) >> 7;
-  return min(max(v, 0), 255);
+  return min(max((__mul24(p, 596864) - 9027848) >> 19, 0), 255);
 }
 
 #define MJG_DESCALE(x, n) (((x) + (1 << ((n) - 1))) >> (n))
@@ -78,20 +78,20 @@ __device__ __forceinline__ void fdct8(int *p) {
     p[0 * S] = MJG_DESCALE(t10 + t11, 4);
     p[4 * S] = MJG_DESCALE(t10 - t11, 4);
   }
-  int z1 = (t12 + t13) * 4433;
-  p[2 * S] = MJG_DESCALE(z1 + t13 * 6270, SH);
-  p[6 * S] = MJG_DESCALE(z1 - t12 * 15137, SH);
+  int z1 = __mul24(t12 + t13, 4433);
+  p[2 * S] = MJG_DESCALE(z1 + __mul24(t13, 6270), SH);
+  p[6 * S] = MJG_DESCALE(z1 - __mul24(t12, 15137), SH);
   z1 = t4 + t7;
   int z2 = t5 + t6, z3 = t4 + t6, z4 = t5 + t7;
-  const int z5 = (z3 + z4) * 9633;
-  t4 *= 2446;
-  t5 *= 16819;
-  t6 *= 25172;
-  t7 *= 12299;
-  z1 *= -7373;
-  z2 *= -20995;
-  z3 *= -16069;
-  z4 *= -3196;
+  const int z5 = __mul24(z3 + z4, 9633);
+  t4 = __mul24(t4, 2446);
+  t5 = __mul24(t5, 16819);
+  t6 = __mul24(t6, 25172);
+  t7 = __mul24(t7, 12299);
+  z1 = __mul24(z1, -7373);
+  z2 = __mul24(z2, -20995);
+  z3 = __mul24(z3, -16069);
+  z4 = __mul24(z4, -3196);
   z3 += z5;
   z4 += z5;
   p[7 * S] = MJG_DESCALE(t4 + z1 + z3, SH);
@@ -113,38 +113,6 @@ __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
   return v;
-}
-
-// Load an 8x8 block at (x0, y0) of a plane with coordinate clamping (FFmpeg
-// emulated_edge_mc / draw_edges replicate the last row/column).
-template <int CHROMA>
-__device__ __forceinline__ void load_block(int (&c)[64], const uint8_t *plane, int stride, int pw,
-                                           int ph, int x0, int y0, int rc) {
-  const uint8_t *base = plane + (size_t)y0 * stride + x0;
-  const bool fast = (x0 + 8 <= pw) && (y0 + 8 <= ph) &&
-                    ((((uintptr_t)base) | (uintptr_t)stride) & 7) == 0;
-  if (fast) {
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      const uint64_t v = __builtin_nontemporal_load((const uint64_t *)(base + (size_t)r * stride));
-#pragma unroll
-      for (int b = 0; b < 8; b++) c[r * 8 + b] = (int)((v >> (8 * b)) & 255u);
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      const int sy = min(y0 + r, ph - 1);
-#pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const int sx = min(x0 + b, pw - 1);
-        c[r * 8 + b] = plane[(size_t)sy * stride + sx];
-      }
-    }
-  }
-  if (rc) {
-#pragma unroll
-    for (int i = 0; i < 64; i++) c[i] = CHROMA ? range_chroma(c[i]) : range_luma(c[i]);
-  }
 }
 
 struct BitSink {
@@ -171,86 +139,206 @@ struct BitSink {
   }
 };
 
-// Huffman coding of one block, FFmpeg mjpegenc.c encode_block / ff_mjpeg_encode_dc.
-// EMIT=false returns the bit length only.
-template <bool EMIT>
-__device__ __forceinline__ uint32_t code_block(const int (&qz)[64], int diff, const uint32_t *ac,
-                                               const uint32_t *dc, BitSink *sink) {
-  uint32_t bits;
-  {
-    const int a = diff < 0 ? -diff : diff;
-    const int cat = diff == 0 ? 0 : 32 - __clz(a);
-    const uint32_t e = dc[cat];
-    bits = (e >> 16) + cat;
-    if (EMIT) {
-      const uint32_t mant = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << cat) - 1u);
-      sink->emit(((e & 0xffffu) << cat) | mant, (int)bits);
+__device__ __forceinline__ int dc_cat(int diff) {
+  const int a = diff < 0 ? -diff : diff;
+  return diff == 0 ? 0 : 32 - __clz(a);
+}
+
+// First emission pass: the block's bits left-aligned in up to 4 register words (a
+// block's offset in the chunk is not known yet); counts every bit even past 4 words.
+struct RegSink {
+  uint64_t acc = 0;
+  int nacc = 0;
+  uint32_t bits = 0, nw = 0;
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  __device__ __forceinline__ void emit(uint32_t v, int n) {
+    acc = (acc << n) | v;
+    nacc += n;
+    bits += (uint32_t)n;
+    if (nacc >= 32) {
+      nacc -= 32;
+      const uint32_t w = (uint32_t)(acc >> nacc);
+      w0 = nw == 0 ? w : w0;
+      w1 = nw == 1 ? w : w1;
+      w2 = nw == 2 ? w : w2;
+      w3 = nw == 3 ? w : w3;
+      nw++;
     }
   }
-  const uint32_t zrl = ac[0xf0];
-  int prev = 0;
-#pragma unroll
-  for (int k = 1; k < 64; k++) {
-    const int v = qz[k];
-    if (v != 0) {
-      int run = k - prev - 1;
-      const int a = v < 0 ? -v : v;
-      const int cat = 32 - __clz(a);
-      const uint32_t e = ac[((run & 15) << 4) | cat];
-      const int len = (int)(e >> 16) + cat;
-      if (EMIT) {
-        while (run >= 16) {
-          sink->emit(zrl & 0xffffu, (int)(zrl >> 16));
-          run -= 16;
-        }
-        const uint32_t mant = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u);
-        sink->emit(((e & 0xffffu) << cat) | mant, len);
-      } else {
-        bits += (uint32_t)(run >> 4) * (zrl >> 16);
-      }
-      bits += len;
-      prev = k;
+  __device__ __forceinline__ void finish() {
+    if (nacc > 0) {
+      const uint32_t w = (uint32_t)(acc << (32 - nacc));
+      w0 = nw == 0 ? w : w0;
+      w1 = nw == 1 ? w : w1;
+      w2 = nw == 2 ? w : w2;
+      w3 = nw == 3 ? w : w3;
+      nw++;
     }
+  }
+};
+
+// Bit-pack one block's Huffman codes, FFmpeg mjpegenc.c encode_block /
+// mjpegenc_common.c ff_mjpeg_encode_dc (ZRL 0xF0 per 16 zeros, EOB unless coef 63 != 0).
+// Walks only the nonzero coefficients (64-bit zigzag mask); coefficients come from the
+// workgroup's LDS block image s_pk[word][thread] (int16 pairs), conflict-free for any
+// per-lane k.
+template <class Sink>
+__device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask, int diff,
+                                           const uint32_t *ac, const uint32_t *dc, Sink &sink) {
+  {
+    const int cat = dc_cat(diff);
+    const uint32_t e = dc[cat];
+    const uint32_t mant = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << cat) - 1u);
+    sink.emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);
+  }
+  int prev = 0;
+  while (mask) {
+    const int k = (int)__builtin_ctzll(mask);
+    mask &= mask - 1;
+    const int v = (int)(int16_t)(pkcol[(k >> 1) * kEncThreads] >> (16 * (k & 1)));
+    int run = k - prev - 1;
+    prev = k;
+    while (run >= 16) {
+      const uint32_t zrl = ac[0xf0];
+      sink.emit(zrl & 0xffffu, (int)(zrl >> 16));
+      run -= 16;
+    }
+    const int a = v < 0 ? -v : v;
+    const int cat = 32 - __clz(a);
+    const uint32_t e = ac[((run & 15) << 4) | cat];
+    const uint32_t mant = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u);
+    sink.emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);
   }
   if (prev != 63) {
     const uint32_t eob = ac[0];
-    bits += eob >> 16;
-    if (EMIT) sink->emit(eob & 0xffffu, (int)(eob >> 16));
+    sink.emit(eob & 0xffffu, (int)(eob >> 16));
   }
-  return bits;
+}
+
+// Raw 8x8 block as 8 little-endian row words.  fetch_rows issues the 8-byte row loads
+// for interior blocks (the prefetch path, 16 VGPRs) and returns false for blocks that
+// touch the frame edge or are misaligned; fetch_rows_edge builds those with
+// coordinate clamping (FFmpeg emulated_edge_mc / draw_edges replicate the last
+// row/column) at a point where no other block data is live.
+struct Src {
+  const uint8_t *plane;
+  int stride, pw, ph, x0, y0;
+};
+
+__device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s) {
+  const uint8_t *base = s.plane + (size_t)s.y0 * s.stride + s.x0;
+  const bool fast = (s.x0 + 8 <= s.pw) && (s.y0 + 8 <= s.ph) &&
+                    ((((uintptr_t)base) | (uintptr_t)s.stride) & 7) == 0;
+  if (fast) {
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+      raw[r] = __builtin_nontemporal_load((const uint64_t *)(base + (size_t)r * s.stride));
+  }
+  return fast;
+}
+
+__device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s) {
+  for (int r = 0; r < 8; r++) {
+    const uint8_t *row = s.plane + (size_t)min(s.y0 + r, s.ph - 1) * s.stride;
+    uint64_t w = 0;
+    for (int b = 0; b < 8; b++) w |= (uint64_t)row[min(s.x0 + b, s.pw - 1)] << (8 * b);
+    raw[r] = w;
+  }
+}
+
+struct Task {
+  int frame, chunk, mcu;
+  bool active;
+};
+
+__device__ __forceinline__ Task make_task(const EncGeom &g, int t, int local_mcu) {
+  Task k;
+  k.frame = t / g.nchunks;
+  k.chunk = t - k.frame * g.nchunks;
+  k.mcu = k.chunk * kMcuPerChunk + local_mcu;
+  k.active = k.mcu < g.nmcu;
+  return k;
+}
+
+__device__ __forceinline__ Src task_src(const uint8_t *frames, const EncGeom &g, const Task &k,
+                                        int blk) {
+  const uint8_t *fr = frames + (size_t)k.frame * g.frame_stride;
+  const int mx = k.mcu % g.mbw, my = k.mcu / g.mbw;
+  Src s;
+  if (blk < 4) {
+    s.plane = fr;
+    s.stride = g.y_stride;
+    s.pw = g.w;
+    s.ph = g.h;
+    s.x0 = mx * 16 + (blk & 1) * 8;
+    s.y0 = my * 16 + (blk >> 1) * 8;
+  } else {
+    s.plane = fr + (blk == 4 ? g.u_off : g.v_off);
+    s.stride = g.c_stride;
+    s.pw = g.cw;
+    s.ph = g.ch;
+    s.x0 = mx * 8;
+    s.y0 = my * 8;
+  }
+  return s;
 }
 
 // ------------------------------------------------------------------ k_encode
-// grid (nchunks, nframes), 384 threads.  Thread roles inside a chunk of 64 MCUs:
+// Persistent grid: workgroup b encodes the contiguous task range [b*T, (b+1)*T) of
+// (frame, chunk) tasks, prefetching the next task's pixels into registers while it
+// encodes the current one.  A task = one chunk of 64 MCUs, 384 threads, one block each:
 //   waves 0,1: Y0/Y1 (top luma row) of MCUs 0-31 / 32-63, lanes interleave Y0,Y1
 //   waves 2,3: Y2/Y3 (bottom luma row), same interleave
 //   wave 4: Cb, wave 5: Cr of MCU = lane
 // so every wave's 8-byte row loads cover 512 contiguous bytes.
+// Per task: [tv->pc] + FDCT in registers -> quantise into the LDS block image + nonzero
+// mask -> DC prediction through LDS -> one Huffman pass over the nonzero coefficients
+// into a 4-word register queue (counting bits) -> block-length scan in MCU order ->
+// queue words OR'ed into a zeroed LDS window at their offsets (blocks over 128 bits
+// re-emit there) -> chunk slot in HBM.
 __global__ __launch_bounds__(kEncThreads) void k_encode(
-    const uint8_t *__restrict__ frames, EncGeom g, QuantTab qt, const uint32_t *__restrict__ tabs,
+    const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
-    int16_t *__restrict__ dbg_coefs) {
+    int16_t *__restrict__ dbg_coefs, int ntasks) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
+  __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ int s_dcq[kEncThreads];
   __shared__ int s_pred[4];
   __shared__ uint32_t s_off[kEncThreads];
   __shared__ uint32_t s_total;
   __shared__ uint32_t s_win[kWinWords];
+  __shared__ uint32_t s_pk[32 * kEncThreads];  // quantised blocks, [word][thread]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int chunk = blockIdx.x, frame = blockIdx.y;
-  const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
+  int local_mcu, blk;
+  if (wave < 4) {
+    local_mcu = 32 * (wave & 1) + (lane >> 1);
+    blk = ((wave >> 1) << 1) | (lane & 1);
+  } else {
+    local_mcu = lane;
+    blk = wave;
+  }
+  const int tab = __builtin_amdgcn_readfirstlane(blk < 4 ? 0 : 1);  // wave-uniform
+  const int per = (ntasks + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(ntasks, t0 + per);
+  if (t0 >= t1) return;
+
+  uint64_t raw[8];
+  Task cur = make_task(g, t0, local_mcu);
+  bool fast = cur.active && fetch_rows(raw, task_src(frames, g, cur, blk));
 
   for (int i = tid; i < 512; i += kEncThreads) s_ac[i] = tabs[i];
   if (tid < 32) s_dc[tid] = tabs[512 + tid];
-
-  // Predecessor DCs (Y3, Cb, Cr of the MCU before this chunk): the quantised DC of a
-  // block is (pixel sum + 32) >> 6 because the FDCT's DC output is the exact sum.
+  if (tid < 64) s_qc[tid] = (int32_t)tabs[544 + tid];
+  for (int i = tid; i < kWinWords; i += kEncThreads) s_win[i] = 0;
+  // Predecessor DCs (Y3, Cb, Cr of the MCU before the first chunk): the quantised DC
+  // of a block is (pixel sum + 32) >> 6 because the FDCT's DC output is the exact sum.
   if (wave < 3) {
-    int dc = 128;
-    if (chunk > 0) {
-      const int m = chunk * kMcuPerChunk - 1;
+    int dcp = 128;
+    if (cur.chunk > 0) {
+      const uint8_t *fr = frames + (size_t)cur.frame * g.frame_stride;
+      const int m = cur.chunk * kMcuPerChunk - 1;
       const int mx = m % g.mbw, my = m / g.mbw;
       const int px = lane & 7, py = lane >> 3;
       int v;
@@ -264,124 +352,172 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(
         v = pl[(size_t)sy * g.c_stride + sx];
         if (g.range_convert) v = range_chroma(v);
       }
-      dc = (wave_sum(v) + 32) >> 6;
+      dcp = (wave_sum(v) + 32) >> 6;
     }
-    if (lane == 0) s_pred[wave] = dc;
+    if (lane == 0) s_pred[wave] = dcp;
   }
-
-  int local_mcu, blk;
-  if (wave < 4) {
-    local_mcu = 32 * (wave & 1) + (lane >> 1);
-    blk = ((wave >> 1) << 1) | (lane & 1);
-  } else {
-    local_mcu = lane;
-    blk = wave;
-  }
-  const int mcu = chunk * kMcuPerChunk + local_mcu;
-  const bool active = mcu < g.nmcu;
-  const int tab = blk < 4 ? 0 : 1;
-
-  int qz[64];
-  int dc = 0;
-  if (active) {
-    const int mx = mcu % g.mbw, my = mcu / g.mbw;
-    int c[64];
-    if (blk < 4) {
-      load_block<0>(c, fr, g.y_stride, g.w, g.h, mx * 16 + (blk & 1) * 8, my * 16 + (blk >> 1) * 8,
-                    g.range_convert);
-    } else {
-      load_block<1>(c, fr + (blk == 4 ? g.u_off : g.v_off), g.c_stride, g.cw, g.ch, mx * 8, my * 8,
-                    g.range_convert);
-    }
-#pragma unroll
-    for (int r = 0; r < 8; r++) fdct8<1, true>(c + r * 8);
-#pragma unroll
-    for (int col = 0; col < 8; col++) fdct8<8, false>(c + col);
-
-    // dct_quantize_c (intra, MJPEG): DC (c+32)/64; AC (|c|*qmat + 3<<18) >> 21, sign
-    // restored, clip_coeffs to +-1023.
-    dc = (c[0] + 32) >> 6;
-    qz[0] = dc;
-#pragma unroll
-    for (int k = 1; k < 64; k++) {
-      const int j = kZigzag[k];
-      const int level = c[j] * qt.qmat[j];
-      const int a = level < 0 ? -level : level;
-      const int q = min((a + (3 << 18)) >> 21, 1023);
-      qz[k] = level < 0 ? -q : q;
-    }
-    if (g.debug_coefs) {
-      int16_t *o = dbg_coefs + (((size_t)frame * g.nmcu + mcu) * 6 + blk) * 64;
-#pragma unroll
-      for (int k = 0; k < 64; k++) o[kZigzag[k]] = (int16_t)qz[k];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 64; k++) qz[k] = 0;
-  }
-  s_dcq[local_mcu * 6 + blk] = dc;
   __syncthreads();
-
-  // DC predictor: previous block of the same component in MCU order (FFmpeg last_dc,
-  // reset to 128 at the start of the frame).
-  int pred;
-  if (blk == 0)
-    pred = local_mcu == 0 ? s_pred[0] : s_dcq[(local_mcu - 1) * 6 + 3];
-  else if (blk < 4)
-    pred = s_dcq[local_mcu * 6 + blk - 1];
-  else
-    pred = local_mcu == 0 ? s_pred[blk - 3] : s_dcq[(local_mcu - 1) * 6 + blk];
-  const int diff = dc - pred;
-
   const uint32_t *ac = s_ac + tab * 256;
   const uint32_t *dct = s_dc + tab * 16;
-  const uint32_t nbits = active ? code_block<false>(qz, diff, ac, dct, nullptr) : 0u;
-  s_off[local_mcu * 6 + blk] = nbits;
-  __syncthreads();
+  const bool rc = g.range_convert != 0;
 
-  // Exclusive scan of the 384 block lengths in MCU order (wave 0: 6 per lane).
-  if (wave == 0) {
-    uint32_t v[6], sum = 0;
+  for (int t = t0; t < t1; t++) {
+    if (cur.active && !fast) fetch_rows_edge(raw, task_src(frames, g, cur, blk));
+    // unpack + tv->pc + FDCT row pass, one row at a time
+    int c[64];
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-      v[i] = s_off[lane * 6 + i];
-      sum += v[i];
-    }
-    const uint32_t incl = wave_incl_scan(sum, lane);
-    uint32_t e = incl - sum;
+    for (int r = 0; r < 8; r++) {
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-      s_off[lane * 6 + i] = e;
-      e += v[i];
+      for (int b = 0; b < 8; b++) {
+        const int p = (int)((raw[r] >> (8 * b)) & 255u);
+        c[r * 8 + b] = !rc ? p : (tab == 0 ? range_luma(p) : range_chroma(p));
+      }
+      fdct8<1, true>(c + r * 8);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (lane == 63) s_total = incl;
-  }
-  __syncthreads();
-  const uint32_t off = s_off[local_mcu * 6 + blk];
-  const uint32_t total = s_total;
-  const uint32_t nwords = (total + 31) >> 5;
-  uint32_t *slot = scratch + ((size_t)frame * g.nchunks + chunk) * kSlotWords;
+    const Task task = cur;
+    if (t + 1 < t1) {  // prefetch the next chunk while this one is encoded
+      cur = make_task(g, t + 1, local_mcu);
+      fast = cur.active && fetch_rows(raw, task_src(frames, g, cur, blk));
+    }
 
-  for (uint32_t wbase = 0; wbase < nwords; wbase += kWinWords) {
-    for (int i = tid; i < kWinWords; i += kEncThreads) s_win[i] = 0;
+    int dc = 0;
+    uint32_t mlo = 0, mhi = 0;
+    if (task.active) {
+      // Column pass, each column quantised as soon as it is done (short live ranges):
+      // dct_quantize_c (intra, MJPEG): DC (c+32)/64; AC (|c|*qmat + 3<<18) >> 21 with the
+      // sign restored.  clip_coeffs (+-1023) never fires: |AC| <= ~6710 for 8-bit input,
+      // so |q| <= (6710 * 2^17 + 3<<18) >> 21 = 419 even at qscale 1.
+      uint16_t *pk16 = (uint16_t *)s_pk;
+#pragma unroll
+      for (int col = 0; col < 8; col++) {
+        __builtin_amdgcn_sched_barrier(0);  // one column in flight at a time
+        fdct8<8, false>(c + col);
+        const int4 qa = *(const int4 *)(s_qc + col * 8), qb = *(const int4 *)(s_qc + col * 8 + 4);
+        const int qm[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const int k = kZigzagInv[r * 8 + col];
+          const int x = c[r * 8 + col];
+          int v;
+          if (k == 0) {
+            dc = (x + 32) >> 6;
+            v = dc;
+          } else {
+            const int ax = x < 0 ? -x : x;
+            const int q = (int)(__umul24((uint32_t)ax, (uint32_t)qm[r]) + (3u << 18)) >> 21;
+            v = x < 0 ? -q : q;
+            if (k < 32)
+              mlo |= q ? (1u << k) : 0u;
+            else
+              mhi |= q ? (1u << (k - 32)) : 0u;
+          }
+          pk16[((k >> 1) * kEncThreads + tid) * 2 + (k & 1)] = (uint16_t)v;
+        }
+      }
+      if (g.debug_coefs) {  // packed zigzag pairs; the host reorders (mjg_debug_coefs)
+        uint32_t *o = (uint32_t *)(dbg_coefs + (((size_t)task.frame * g.nmcu + task.mcu) * 6 + blk) * 64);
+#pragma unroll
+        for (int k = 0; k < 32; k++) o[k] = s_pk[k * kEncThreads + tid];
+      }
+    }
+    const uint64_t mask = ((uint64_t)mhi << 32) | mlo;
+    s_dcq[local_mcu * 6 + blk] = dc;
     __syncthreads();
-    const uint32_t first_w = off >> 5, last_w = (off + nbits - 1) >> 5;
-    if (active && last_w >= wbase && first_w < wbase + kWinWords) {
-      BitSink sink;
-      sink.acc = 0;
-      sink.nacc = (int)(off & 31);
-      sink.widx = first_w;
-      sink.wbase = wbase;
-      sink.win = s_win;
-      code_block<true>(qz, diff, ac, dct, &sink);
-      sink.finish();
+
+    // DC predictor: previous block of the same component in MCU order (FFmpeg
+    // last_dc, reset to 128 at the start of every frame).
+    int pred;
+    if (blk == 0)
+      pred = local_mcu == 0 ? s_pred[0] : s_dcq[(local_mcu - 1) * 6 + 3];
+    else if (blk < 4)
+      pred = s_dcq[local_mcu * 6 + blk - 1];
+    else
+      pred = local_mcu == 0 ? s_pred[blk - 3] : s_dcq[(local_mcu - 1) * 6 + blk];
+    const int diff = dc - pred;
+    RegSink q;
+#if MJG_ABLATE == 0
+    if (task.active) {
+      emit_block(s_pk + tid, mask, diff, ac, dct, q);
+      q.finish();
+    }
+#else
+    if (task.active) {
+      q.emit((uint32_t)mask & 0xffffu, 16);
+      q.finish();
+    }
+#endif
+    s_off[local_mcu * 6 + blk] = q.bits;
+    __syncthreads();
+
+    // Exclusive scan of the 384 block lengths in MCU order (wave 0: 6 per lane); wave 1
+    // hands the chunk's last Y3/Cb/Cr DCs to the next task of this workgroup.
+    if (wave == 0) {
+      uint32_t v[6], sum = 0;
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        v[i] = s_off[lane * 6 + i];
+        sum += v[i];
+      }
+      const uint32_t incl = wave_incl_scan(sum, lane);
+      uint32_t e = incl - sum;
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        s_off[lane * 6 + i] = e;
+        e += v[i];
+      }
+      if (lane == 63) s_total = incl;
+    } else if (wave == 1 && lane < 3) {
+      const bool frame_end = task.chunk == g.nchunks - 1;
+      s_pred[lane] = frame_end ? 128 : s_dcq[63 * 6 + 3 + lane];
     }
     __syncthreads();
-    const uint32_t n = min((uint32_t)kWinWords, nwords - wbase);
-    for (uint32_t i = tid; i < n; i += kEncThreads) slot[wbase + i] = s_win[i];
-    __syncthreads();
+    const uint32_t off = s_off[local_mcu * 6 + blk];
+    const uint32_t total = s_total;
+    const uint32_t nwords = (total + 31) >> 5;
+    uint32_t *slot = scratch + (size_t)t * kSlotWords;
+
+    for (uint32_t wbase = 0; wbase < nwords; wbase += kWinWords) {
+      if (wbase) {  // only for chunks above kWinWords words of bits
+        for (int i = tid; i < kWinWords; i += kEncThreads) s_win[i] = 0;
+        __syncthreads();
+      }
+      const uint32_t first_w = off >> 5, last_w = (off + q.bits - 1) >> 5;
+      if (task.active && last_w >= wbase && first_w < wbase + kWinWords) {
+        if (q.bits <= 128) {
+          // shift the queued words to the block's offset: up to 5 destination words
+          const uint32_t s = off & 31;
+          const uint32_t w[4] = {q.w0, q.w1, q.w2, q.w3};
+#pragma unroll
+          for (int i = 0; i < 5; i++) {
+            if ((uint32_t)i <= last_w - first_w) {
+              const uint32_t hi = i < 4 ? (s ? w[i] >> s : w[i]) : 0u;
+              const uint32_t lo = (i > 0 && s) ? w[i - 1] << (32 - s) : 0u;
+              const uint32_t idx = first_w + i - wbase;
+              if (idx < (uint32_t)kWinWords) atomicOr(&s_win[idx], hi | lo);
+            }
+          }
+        } else {  // long block: re-emit straight into the window at its offset
+          BitSink sink;
+          sink.acc = 0;
+          sink.nacc = (int)(off & 31);
+          sink.widx = first_w;
+          sink.wbase = wbase;
+          sink.win = s_win;
+          emit_block(s_pk + tid, mask, diff, ac, dct, sink);
+          sink.finish();
+        }
+      }
+      __syncthreads();
+      const uint32_t n = min((uint32_t)kWinWords, nwords - wbase);
+      for (uint32_t i = tid; i < n; i += kEncThreads) {
+        slot[wbase + i] = s_win[i];
+        s_win[i] = 0;  // ready for the next task
+      }
+      __syncthreads();
+    }
+    if (tid == 0) chunk_bits[t] = total;
   }
-  if (tid == 0) chunk_bits[(size_t)frame * g.nchunks + chunk] = total;
 }
 
 // --------------------------------------------------------------- block scan

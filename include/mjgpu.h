@@ -107,6 +107,15 @@ int mjg_host_free(void *ptr);
  * and the number of submits it was averaged over.  Needs MJG_F_TIMING. */
 int mjg_kernel_times(mjg_ctx *ctx, double *ms /* [MJG_NUM_KERNELS] */, int *launches, int reset);
 
+/* Device-free helpers (no HIP call; usable on a host without a GPU). */
+/* The per-config JPEG header (SOI .. SOS) for cfg (only dst_w/dst_h/qscale/sar are read). */
+int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *len);
+/* swscale bicubic filter table the scale stage applies: one = 1<<14 (horizontal) or 1<<12
+ * (vertical); align = 4 / 2 (x86 swscale); pos = swscale local position (128 = centred).
+ * coeff receives dst_len*taps int16, pos_out dst_len int32; query taps with coeff == NULL. */
+int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, int src_pos,
+                   int dst_pos, int16_t *coeff, size_t coeff_cap, int32_t *pos_out, int *taps);
+
 /* Test hooks (tests/ only). */
 /* Quantized coefficients (natural order) of frame `frame` of the last submit, blocks
  * in MCU order (Y0 Y1 Y2 Y3 Cb Cr per MCU).  Needs MJG_F_DEBUG_COEFS. */
