@@ -258,7 +258,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   g.ch = ch;
   g.mbw = (w + 15) / 16;
   g.nmcu = g.mbw * ((h + 15) / 16);
-  g.nchunks = (g.nmcu + kMcuPerChunk - 1) / kMcuPerChunk;
+  g.nchunks = (g.nmcu * 6 + 63) / 64;  // chunks of 64 blocks (one wave each)
   g.y_stride = w;
   g.c_stride = cw;
   g.u_off = (long long)w * h;
@@ -328,7 +328,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // persistent k_encode grid: every CU filled with as many workgroups as fit
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode, kEncThreads, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode, 64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
 
   c->timing = (k.flags & MJG_F_TIMING) != 0;
@@ -346,12 +346,14 @@ void tmark(mjg_ctx *c, int k, int end) {
 
 int launch_write(mjg_ctx *c, int n) {
   const EncGeom &g = c->geom;
+  const int ntasks = g.nchunks * n;
   HIP_TRY(hipMemsetAsync(c->d_status, 0, 4, c->stream));
   tmark(c, MJG_K_WRITE, 0);
-  k_write<<<dim3(g.nchunks, n), 256, 0, c->stream>>>(
+  k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
+                                       (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status);
+  k_write<<<(ntasks + 255) / 256, 256, 0, c->stream>>>(
       c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
-      c->d_hdr, (int)c->hdr.size(), g.nchunks, c->d_out, (uint64_t)c->out_cap, c->d_frame_offsets,
-      c->d_status);
+      c->d_frame_offsets, (int)c->hdr.size(), g.nchunks, ntasks, c->d_out, (uint64_t)c->out_cap);
   tmark(c, MJG_K_WRITE, 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->h_sizes, c->d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -443,8 +445,9 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   }
   tmark(c, MJG_K_ENCODE, 0);
   const int ntasks = g.nchunks * n;
-  k_encode<<<std::min(ntasks, c->enc_grid), kEncThreads, 0, c->stream>>>(
-      enc_in, g, c->d_tabs, c->d_scratch, c->d_chunk_bits, c->d_dbg, ntasks);
+  const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
+  k_encode<<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
+                                                    c->d_chunk_bits, c->d_dbg, ntasks);
   tmark(c, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_BITS, 0);
@@ -452,8 +455,9 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_COUNT_FF, 0);
-  k_count_ff<<<dim3(g.nchunks, n), 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits, c->d_chunk_off,
-                                                        c->d_frame_bits, c->d_chunk_ff, g.nchunks);
+  k_count_ff<<<(ntasks + 255) / 256, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits,
+                                                          c->d_chunk_off, c->d_frame_bits,
+                                                          c->d_chunk_ff, g.nchunks, ntasks);
   tmark(c, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_FF, 0);
@@ -589,7 +593,7 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   if (!c->d_dbg) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
   int rc = mjg_sync(c, nullptr, nullptr);
   if (rc) return rc;
-  const size_t nb = (size_t)c->geom.nmcu * 6;
+  const size_t nb = (size_t)c->geom.nmcu * 6;  // dbg buffer: frame-major, block order
   if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
   std::vector<int16_t> zz(nb * 64);  // kernel stores zigzag order

@@ -27,11 +27,8 @@
 
 namespace mjg {
 
-constexpr int kMcuPerChunk = 64;
-constexpr int kEncThreads = 6 * 64;  // 6 blocks per MCU x 64 MCUs, one block per thread
-constexpr int kWinWords = 2048;      // LDS bit-pack window (8 KiB)
 constexpr int kMaxBlockBits = 1664;  // >= DC 16 + 63 * (16 + 10) bits
-constexpr int kSlotWords = (kMcuPerChunk * 6 * kMaxBlockBits + 31) / 32;
+constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 blocks
 
 struct EncGeom {
   int w, h;            // encoded size
@@ -100,6 +97,13 @@ __device__ __forceinline__ void fdct8(int *p) {
   p[1 * S] = MJG_DESCALE(t7 + z1 + z4, SH);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
+// (lgkmcnt) but NOT for outstanding global loads, so a prefetch issued before the
+// barrier stays in flight (__syncthreads() would add s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -121,9 +125,10 @@ struct BitSink {
   uint32_t widx;   // chunk-relative index of the word being filled
   uint32_t wbase;  // first word of the LDS window
   uint32_t *win;
+  uint32_t cap;    // window size in words
   __device__ __forceinline__ void put(uint32_t w) {
     const uint32_t i = widx - wbase;
-    if (i < (uint32_t)kWinWords) atomicOr(&win[i], w);
+    if (i < cap) atomicOr(&win[i], w);
     widx++;
   }
   __device__ __forceinline__ void emit(uint32_t v, int n) {
@@ -182,7 +187,7 @@ struct RegSink {
 // Walks only the nonzero coefficients (64-bit zigzag mask); coefficients come from the
 // workgroup's LDS block image s_pk[word][thread] (int16 pairs), conflict-free for any
 // per-lane k.
-template <class Sink>
+template <int STRIDE, class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask, int diff,
                                            const uint32_t *ac, const uint32_t *dc, Sink &sink) {
   {
@@ -195,7 +200,7 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask,
   while (mask) {
     const int k = (int)__builtin_ctzll(mask);
     mask &= mask - 1;
-    const int v = (int)(int16_t)(pkcol[(k >> 1) * kEncThreads] >> (16 * (k & 1)));
+    const int v = (int)(int16_t)(pkcol[(k >> 1) * STRIDE] >> (16 * (k & 1)));
     int run = k - prev - 1;
     prev = k;
     while (run >= 16) {
@@ -246,24 +251,26 @@ __device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s
   }
 }
 
-struct Task {
-  int frame, chunk, mcu;
-  bool active;
-};
+// ------------------------------------------------------------------ k_encode
+// Wave-granular chunks, no workgroup barriers.  A chunk is 64 consecutive blocks of a
+// frame in MCU-interleaved order (Y0 Y1 Y2 Y3 Cb Cr per MCU), lane = block, so a wave
+// owns a contiguous piece of the frame's bitstream:
+//   * DC prediction: the predecessor of block b is b-3 (Y0), b-1 (Y1..Y3) or b-6 (Cb,
+//     Cr) -- a lane shuffle, or the previous chunk's DCs carried in a register (this
+//     wave encoded that chunk in its previous iteration; the first chunk of a wave's
+//     range recomputes them from pixel sums: quantised DC = (sum + 32) >> 6 exactly);
+//   * bit offsets: wave prefix-sum of the 64 block lengths;
+//   * bit-packing: ds_or_b32 into the wave's private LDS window, then coalesced stores
+//     of the chunk's words to its HBM slot.
+// Persistent grid: wave w encodes chunks [w*T, (w+1)*T) in (frame, chunk) order and
+// prefetches the next chunk's pixel rows into registers while encoding the current one.
+constexpr int kWavesPerWg = 4;
+constexpr int kWaveWinWords = 512;  // per-wave bit-pack window (2 KiB); heavier chunks loop
 
-__device__ __forceinline__ Task make_task(const EncGeom &g, int t, int local_mcu) {
-  Task k;
-  k.frame = t / g.nchunks;
-  k.chunk = t - k.frame * g.nchunks;
-  k.mcu = k.chunk * kMcuPerChunk + local_mcu;
-  k.active = k.mcu < g.nmcu;
-  return k;
-}
-
-__device__ __forceinline__ Src task_src(const uint8_t *frames, const EncGeom &g, const Task &k,
-                                        int blk) {
-  const uint8_t *fr = frames + (size_t)k.frame * g.frame_stride;
-  const int mx = k.mcu % g.mbw, my = k.mcu / g.mbw;
+__device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g, int frame, int b) {
+  const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
+  const int m = b / 6, blk = b - 6 * (b / 6);
+  const int mx = m % g.mbw, my = m / g.mbw;
   Src s;
   if (blk < 4) {
     s.plane = fr;
@@ -283,107 +290,90 @@ __device__ __forceinline__ Src task_src(const uint8_t *frames, const EncGeom &g,
   return s;
 }
 
-// ------------------------------------------------------------------ k_encode
-// Persistent grid: workgroup b encodes the contiguous task range [b*T, (b+1)*T) of
-// (frame, chunk) tasks, prefetching the next task's pixels into registers while it
-// encodes the current one.  A task = one chunk of 64 MCUs, 384 threads, one block each:
-//   waves 0,1: Y0/Y1 (top luma row) of MCUs 0-31 / 32-63, lanes interleave Y0,Y1
-//   waves 2,3: Y2/Y3 (bottom luma row), same interleave
-//   wave 4: Cb, wave 5: Cr of MCU = lane
-// so every wave's 8-byte row loads cover 512 contiguous bytes.
-// Per task: [tv->pc] + FDCT in registers -> quantise into the LDS block image + nonzero
-// mask -> DC prediction through LDS -> one Huffman pass over the nonzero coefficients
-// into a 4-word register queue (counting bits) -> block-length scan in MCU order ->
-// queue words OR'ed into a zeroed LDS window at their offsets (blocks over 128 bits
-// re-emit there) -> chunk slot in HBM.
-__global__ __launch_bounds__(kEncThreads) void k_encode(
+__global__ __launch_bounds__(64 * kWavesPerWg) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, int ntasks) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
-  __shared__ int s_dcq[kEncThreads];
-  __shared__ int s_pred[4];
-  __shared__ uint32_t s_off[kEncThreads];
-  __shared__ uint32_t s_total;
-  __shared__ uint32_t s_win[kWinWords];
-  __shared__ uint32_t s_pk[32 * kEncThreads];  // quantised blocks, [word][thread]
+  __shared__ uint32_t s_win_all[kWavesPerWg][kWaveWinWords];
+  __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  int local_mcu, blk;
-  if (wave < 4) {
-    local_mcu = 32 * (wave & 1) + (lane >> 1);
-    blk = ((wave >> 1) << 1) | (lane & 1);
-  } else {
-    local_mcu = lane;
-    blk = wave;
-  }
-  const int tab = __builtin_amdgcn_readfirstlane(blk < 4 ? 0 : 1);  // wave-uniform
-  const int per = (ntasks + gridDim.x - 1) / gridDim.x;
-  const int t0 = blockIdx.x * per, t1 = min(ntasks, t0 + per);
-  if (t0 >= t1) return;
-
-  uint64_t raw[8];
-  Task cur = make_task(g, t0, local_mcu);
-  bool fast = cur.active && fetch_rows(raw, task_src(frames, g, cur, blk));
-
-  for (int i = tid; i < 512; i += kEncThreads) s_ac[i] = tabs[i];
+  for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
   if (tid < 32) s_dc[tid] = tabs[512 + tid];
   if (tid < 64) s_qc[tid] = (int32_t)tabs[544 + tid];
-  for (int i = tid; i < kWinWords; i += kEncThreads) s_win[i] = 0;
-  // Predecessor DCs (Y3, Cb, Cr of the MCU before the first chunk): the quantised DC
-  // of a block is (pixel sum + 32) >> 6 because the FDCT's DC output is the exact sum.
-  if (wave < 3) {
-    int dcp = 128;
-    if (cur.chunk > 0) {
-      const uint8_t *fr = frames + (size_t)cur.frame * g.frame_stride;
-      const int m = cur.chunk * kMcuPerChunk - 1;
-      const int mx = m % g.mbw, my = m / g.mbw;
-      const int px = lane & 7, py = lane >> 3;
-      int v;
-      if (wave == 0) {
-        const int sx = min(mx * 16 + 8 + px, g.w - 1), sy = min(my * 16 + 8 + py, g.h - 1);
-        v = fr[(size_t)sy * g.y_stride + sx];
-        if (g.range_convert) v = range_luma(v);
-      } else {
-        const uint8_t *pl = fr + (wave == 1 ? g.u_off : g.v_off);
-        const int sx = min(mx * 8 + px, g.cw - 1), sy = min(my * 8 + py, g.ch - 1);
-        v = pl[(size_t)sy * g.c_stride + sx];
-        if (g.range_convert) v = range_chroma(v);
-      }
-      dcp = (wave_sum(v) + 32) >> 6;
-    }
-    if (lane == 0) s_pred[wave] = dcp;
-  }
-  __syncthreads();
-  const uint32_t *ac = s_ac + tab * 256;
-  const uint32_t *dct = s_dc + tab * 16;
+  uint32_t *s_win = s_win_all[wave];
+  uint32_t *s_pk = s_pk_all[wave];
+  for (int i = lane; i < kWaveWinWords; i += 64) s_win[i] = 0;
+  __syncthreads();  // tables visible; the only workgroup barrier
+
+  const int nwaves = gridDim.x * kWavesPerWg;
+  const int gw = blockIdx.x * kWavesPerWg + wave;
+  const int per = (ntasks + nwaves - 1) / nwaves;
+  const int t0 = gw * per, t1 = min(ntasks, t0 + per);
+  if (t0 >= t1) return;
+  const int nblk = g.nmcu * 6;
+  const int nck = (nblk + 63) >> 6;
   const bool rc = g.range_convert != 0;
 
+  // first chunk of this wave's range
+  int frame = t0 / nck, chunk = t0 - frame * nck;
+  int b = chunk * 64 + lane;
+  bool active = b < nblk;
+  uint64_t raw[8];
+  bool fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
+
+  // DC carry: quantised DCs of the 64 blocks before this chunk (lane i = block chunk*64-64+i)
+  int carry = 128;
+  if (chunk > 0) {
+    for (int i = 0; i < 6; i++) {  // only blocks chunk*64-6 .. -1 can be predecessors
+      const int pb = chunk * 64 - 6 + i;
+      const Src s = block_src(frames, g, frame, pb);
+      const int px = lane & 7, py = lane >> 3;
+      int v = s.plane[(size_t)min(s.y0 + py, s.ph - 1) * s.stride + min(s.x0 + px, s.pw - 1)];
+      const int chroma = (pb - 6 * (pb / 6)) >= 4;
+      if (rc) v = chroma ? range_chroma(v) : range_luma(v);
+      const int d = (wave_sum(v) + 32) >> 6;
+      if (lane == 58 + i) carry = d;
+    }
+  }
+
   for (int t = t0; t < t1; t++) {
-    if (cur.active && !fast) fetch_rows_edge(raw, task_src(frames, g, cur, blk));
-    // unpack + tv->pc + FDCT row pass, one row at a time
+    const int blk = b - 6 * (b / 6);
+    const int tab = blk < 4 ? 0 : 1;
+    if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, b));
+    // unpack + tv->pc + FDCT row pass, one row at a time.  Luma and chroma share one
+    // formula: chroma's (p*596864 - 9027848) >> 19 == (p*2387456 - 36111392) >> 21.
+    const int rmul = tab ? 2387456 : 2441856, radd = tab ? 36111392 : 38008785;
     int c[64];
 #pragma unroll
     for (int r = 0; r < 8; r++) {
 #pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const int p = (int)((raw[r] >> (8 * b)) & 255u);
-        c[r * 8 + b] = !rc ? p : (tab == 0 ? range_luma(p) : range_chroma(p));
+      for (int x = 0; x < 8; x++) {
+        const int p = (int)((raw[r] >> (8 * x)) & 255u);
+        c[r * 8 + x] = !rc ? p : min(max((__mul24(p, rmul) - radd) >> 21, 0), 255);
       }
       fdct8<1, true>(c + r * 8);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const Task task = cur;
-    if (t + 1 < t1) {  // prefetch the next chunk while this one is encoded
-      cur = make_task(g, t + 1, local_mcu);
-      fast = cur.active && fetch_rows(raw, task_src(frames, g, cur, blk));
+    // prefetch the next chunk while this one is encoded
+    const int cur_frame = frame, cur_chunk = chunk;
+    const bool cur_active = active;
+    if (t + 1 < t1) {
+      if (++chunk == nck) {
+        chunk = 0;
+        frame++;
+      }
+      b = chunk * 64 + lane;
+      active = b < nblk;
+      fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
     }
 
     int dc = 0;
     uint32_t mlo = 0, mhi = 0;
-    if (task.active) {
+    if (cur_active) {
       // Column pass, each column quantised as soon as it is done (short live ranges):
       // dct_quantize_c (intra, MJPEG): DC (c+32)/64; AC (|c|*qmat + 3<<18) >> 21 with the
       // sign restored.  clip_coeffs (+-1023) never fires: |AC| <= ~6710 for 8-bit input,
@@ -412,78 +402,47 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(
             else
               mhi |= q ? (1u << (k - 32)) : 0u;
           }
-          pk16[((k >> 1) * kEncThreads + tid) * 2 + (k & 1)] = (uint16_t)v;
+          pk16[((k >> 1) * 64 + lane) * 2 + (k & 1)] = (uint16_t)v;
         }
       }
       if (g.debug_coefs) {  // packed zigzag pairs; the host reorders (mjg_debug_coefs)
-        uint32_t *o = (uint32_t *)(dbg_coefs + (((size_t)task.frame * g.nmcu + task.mcu) * 6 + blk) * 64);
+        uint32_t *o = (uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64);
 #pragma unroll
-        for (int k = 0; k < 32; k++) o[k] = s_pk[k * kEncThreads + tid];
+        for (int k = 0; k < 32; k++) o[k] = s_pk[k * 64 + lane];
       }
     }
     const uint64_t mask = ((uint64_t)mhi << 32) | mlo;
-    s_dcq[local_mcu * 6 + blk] = dc;
-    __syncthreads();
 
-    // DC predictor: previous block of the same component in MCU order (FFmpeg
-    // last_dc, reset to 128 at the start of every frame).
-    int pred;
-    if (blk == 0)
-      pred = local_mcu == 0 ? s_pred[0] : s_dcq[(local_mcu - 1) * 6 + 3];
-    else if (blk < 4)
-      pred = s_dcq[local_mcu * 6 + blk - 1];
-    else
-      pred = local_mcu == 0 ? s_pred[blk - 3] : s_dcq[(local_mcu - 1) * 6 + blk];
+    // DC predictor (FFmpeg last_dc, 128 at every frame start): shuffle within the chunk,
+    // else the carried DCs of the previous chunk.
+    const int delta = blk == 0 ? 3 : (blk < 4 ? 1 : 6);
+    const int src_lane = (lane - delta) & 63;
+    const int from_cur = __shfl(dc, src_lane, 64), from_prev = __shfl(carry, src_lane, 64);
+    const int pred = lane >= delta ? from_cur : (cur_chunk == 0 ? 128 : from_prev);
     const int diff = dc - pred;
+    carry = dc;
+
     RegSink q;
 #if MJG_ABLATE == 0
-    if (task.active) {
-      emit_block(s_pk + tid, mask, diff, ac, dct, q);
+    if (cur_active) {
+      emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, q);
       q.finish();
     }
 #else
-    if (task.active) {
+    if (cur_active) {
       q.emit((uint32_t)mask & 0xffffu, 16);
       q.finish();
     }
 #endif
-    s_off[local_mcu * 6 + blk] = q.bits;
-    __syncthreads();
-
-    // Exclusive scan of the 384 block lengths in MCU order (wave 0: 6 per lane); wave 1
-    // hands the chunk's last Y3/Cb/Cr DCs to the next task of this workgroup.
-    if (wave == 0) {
-      uint32_t v[6], sum = 0;
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        v[i] = s_off[lane * 6 + i];
-        sum += v[i];
-      }
-      const uint32_t incl = wave_incl_scan(sum, lane);
-      uint32_t e = incl - sum;
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        s_off[lane * 6 + i] = e;
-        e += v[i];
-      }
-      if (lane == 63) s_total = incl;
-    } else if (wave == 1 && lane < 3) {
-      const bool frame_end = task.chunk == g.nchunks - 1;
-      s_pred[lane] = frame_end ? 128 : s_dcq[63 * 6 + 3 + lane];
-    }
-    __syncthreads();
-    const uint32_t off = s_off[local_mcu * 6 + blk];
-    const uint32_t total = s_total;
+    const uint32_t incl = wave_incl_scan(q.bits, lane);
+    const uint32_t off = incl - q.bits;
+    const uint32_t total = __shfl(incl, 63, 64);
     const uint32_t nwords = (total + 31) >> 5;
     uint32_t *slot = scratch + (size_t)t * kSlotWords;
 
-    for (uint32_t wbase = 0; wbase < nwords; wbase += kWinWords) {
-      if (wbase) {  // only for chunks above kWinWords words of bits
-        for (int i = tid; i < kWinWords; i += kEncThreads) s_win[i] = 0;
-        __syncthreads();
-      }
+    for (uint32_t wbase = 0; wbase < nwords; wbase += kWaveWinWords) {
       const uint32_t first_w = off >> 5, last_w = (off + q.bits - 1) >> 5;
-      if (task.active && last_w >= wbase && first_w < wbase + kWinWords) {
+      if (cur_active && last_w >= wbase && first_w < wbase + kWaveWinWords) {
         if (q.bits <= 128) {
           // shift the queued words to the block's offset: up to 5 destination words
           const uint32_t s = off & 31;
@@ -494,7 +453,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(
               const uint32_t hi = i < 4 ? (s ? w[i] >> s : w[i]) : 0u;
               const uint32_t lo = (i > 0 && s) ? w[i - 1] << (32 - s) : 0u;
               const uint32_t idx = first_w + i - wbase;
-              if (idx < (uint32_t)kWinWords) atomicOr(&s_win[idx], hi | lo);
+              if (idx < (uint32_t)kWaveWinWords) atomicOr(&s_win[idx], hi | lo);
             }
           }
         } else {  // long block: re-emit straight into the window at its offset
@@ -504,19 +463,18 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(
           sink.widx = first_w;
           sink.wbase = wbase;
           sink.win = s_win;
-          emit_block(s_pk + tid, mask, diff, ac, dct, sink);
+          sink.cap = kWaveWinWords;
+          emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, sink);
           sink.finish();
         }
       }
-      __syncthreads();
-      const uint32_t n = min((uint32_t)kWinWords, nwords - wbase);
-      for (uint32_t i = tid; i < n; i += kEncThreads) {
+      const uint32_t n = min((uint32_t)kWaveWinWords, nwords - wbase);
+      for (uint32_t i = lane; i < n; i += 64) {
         slot[wbase + i] = s_win[i];
-        s_win[i] = 0;  // ready for the next task
+        s_win[i] = 0;  // ready for the next window / chunk
       }
-      __syncthreads();
     }
-    if (tid == 0) chunk_bits[t] = total;
+    if (lane == 0) chunk_bits[t] = total;
   }
 }
 
@@ -603,26 +561,24 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
+// Thread per chunk: realign the chunk's words to its frame offset and count the 0xFF
+// bytes among the bytes it owns (a byte belongs to the chunk holding its first bit).
 __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
                                                   const uint32_t *__restrict__ chunk_bits,
                                                   const uint32_t *__restrict__ chunk_off,
                                                   const uint32_t *__restrict__ frame_bits,
-                                                  uint32_t *__restrict__ chunk_ff, int nchunks) {
-  __shared__ int s_w[4];
-  const int c = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-  const size_t ci = (size_t)f * nchunks + c;
-  const uint32_t O = chunk_off[ci], L = chunk_bits[ci], T = frame_bits[f];
+                                                  uint32_t *__restrict__ chunk_ff, int nchunks,
+                                                  int ntotal) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ntotal) return;
+  const int f = i / nchunks, c = i - f * nchunks;
+  const uint32_t O = chunk_off[i], L = chunk_bits[i], T = frame_bits[f];
   const uint32_t total_bytes = (T + 7) >> 3;
   const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-  int cnt = 0;
-  for (uint32_t k = k0 + tid; k < k1; k += 256) {
-    const uint32_t v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
-    cnt += ff_in_word(v, 4 * k, total_bytes);
-  }
-  cnt = wave_sum(cnt);
-  if ((tid & 63) == 0) s_w[tid >> 6] = cnt;
-  __syncthreads();
-  if (tid == 0) chunk_ff[ci] = (uint32_t)(s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+  uint32_t cnt = 0;
+  for (uint32_t k = k0; k < k1; k++)
+    cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k), 4 * k, total_bytes);
+  chunk_ff[i] = cnt;
 }
 
 __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ chunk_ff,
@@ -636,81 +592,62 @@ __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ c
   if (threadIdx.x == 0) frame_size[f] = (uint64_t)hdr_len + ((frame_bits[f] + 7) >> 3) + t + 2;
 }
 
-// grid (nchunks, nframes), 256 threads.  Writes chunk c's owned bytes with a 0x00 after
-// every 0xFF; chunk 0 also writes the header, the last chunk the EOI marker.
+// One wave per frame: packed output offset (sum of the preceding frame sizes), capacity
+// check, header (SOI .. SOS) and EOI of the frame.
+__global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ frame_size,
+                                                  const uint8_t *__restrict__ hdr, int hdr_len,
+                                                  uint8_t *__restrict__ out, uint64_t out_cap,
+                                                  uint64_t *__restrict__ frame_offsets,
+                                                  uint32_t *__restrict__ status) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  uint64_t s = 0;
+  for (int i = lane; i < f; i += 64) s += frame_size[i];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  const uint64_t fsize = frame_size[f];
+  if (lane == 0) {
+    frame_offsets[f] = s;
+    if (f == (int)gridDim.x - 1) frame_offsets[f + 1] = s + fsize;
+  }
+  if (s + fsize > out_cap) {
+    if (lane == 0) atomicOr(status, 1u);
+    return;
+  }
+  uint8_t *fo = out + s;
+  for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
+  if (lane == 0) {
+    fo[fsize - 2] = 0xff;
+    fo[fsize - 1] = 0xd9;
+  }
+}
+
+// Thread per chunk: the chunk's owned bytes, a 0x00 after every 0xFF
+// (ff_mjpeg_escape_FF), at header + unstuffed position + 0xFFs before it in the frame.
 __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
     const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
     const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
-    const uint8_t *__restrict__ hdr, int hdr_len, int nchunks, uint8_t *__restrict__ out,
-    uint64_t out_cap, uint64_t *__restrict__ frame_offsets, uint32_t *__restrict__ status) {
-  __shared__ uint32_t s_w[4];
-  __shared__ uint64_t s_foff;
-  __shared__ uint32_t s_carry;
-  const int c = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (wave == 0) {
-    uint64_t s = 0;
-    for (int i = lane; i < f; i += 64) s += frame_size[i];
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
-    if (lane == 0) {
-      s_foff = s;
-      s_carry = 0;
-    }
-  }
-  __syncthreads();
-  const uint64_t foff = s_foff;
-  const uint64_t fsize = frame_size[f];
-  if (foff + fsize > out_cap) {
-    if (tid == 0) atomicOr(status, 1u);
-    return;
-  }
-  if (c == 0 && tid == 0) {
-    frame_offsets[f] = foff;
-    if (f == (int)gridDim.y - 1) frame_offsets[f + 1] = foff + fsize;
-  }
-  uint8_t *fo = out + foff;
-  if (c == 0)
-    for (int i = tid; i < hdr_len; i += 256) fo[i] = hdr[i];
-  const size_t ci = (size_t)f * nchunks + c;
-  const uint32_t O = chunk_off[ci], L = chunk_bits[ci], T = frame_bits[f];
+    const uint64_t *__restrict__ frame_offsets, int hdr_len, int nchunks, int ntotal,
+    uint8_t *__restrict__ out, uint64_t out_cap) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ntotal) return;
+  const int f = i / nchunks, c = i - f * nchunks;
+  const uint64_t foff = frame_offsets[f];
+  if (foff + frame_size[f] > out_cap) return;  // k_frame_hdr flagged the overflow
+  const uint32_t O = chunk_off[i], L = chunk_bits[i], T = frame_bits[f];
   const uint32_t total_bytes = (T + 7) >> 3;
-  if (c == nchunks - 1 && tid == 0) {
-    fo[fsize - 2] = 0xff;
-    fo[fsize - 1] = 0xd9;
-  }
   const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-  uint8_t *scan = fo + hdr_len;
-  const uint32_t ff_before = ff_off[ci];
-  for (uint32_t kb = k0; kb < k1; kb += 256) {
-    const uint32_t k = kb + tid;
-    uint32_t v = 0;
-    int cnt = 0;
-    if (k < k1) {
-      v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
-      cnt = ff_in_word(v, 4 * k, total_bytes);
-    }
-    const uint32_t incl = wave_incl_scan((uint32_t)cnt, lane);
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t wpre = 0;
-    for (int i = 0; i < wave; i++) wpre += s_w[i];
-    const uint32_t carry = s_carry;
-    if (k < k1) {
-      // stuffed position of this word's first byte
-      uint32_t pos = 4 * k + ff_before + carry + wpre + incl - (uint32_t)cnt;
+  uint8_t *p = out + foff + hdr_len + 4 * (size_t)k0 + ff_off[i];
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint32_t v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
-        if (4 * k + b < total_bytes) {
-          const uint8_t byte = (uint8_t)(v >> (24 - 8 * b));
-          scan[pos++] = byte;
-          if (byte == 0xff) scan[pos++] = 0;
-        }
+    for (int bb = 0; bb < 4; bb++) {
+      if (4 * k + bb < total_bytes) {
+        const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
+        *p++ = byte;
+        if (byte == 0xff) *p++ = 0;
       }
     }
-    __syncthreads();
-    if (tid == 255) s_carry = carry + s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    __syncthreads();
   }
 }
 
