@@ -351,7 +351,7 @@ int launch_write(mjg_ctx *c, int n) {
   tmark(c, MJG_K_WRITE, 0);
   k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
                                        (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status);
-  k_write<<<(ntasks + 255) / 256, 256, 0, c->stream>>>(
+  k_write<<<(ntasks + 3) / 4, 256, 0, c->stream>>>(
       c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
       c->d_frame_offsets, (int)c->hdr.size(), g.nchunks, ntasks, c->d_out, (uint64_t)c->out_cap);
   tmark(c, MJG_K_WRITE, 1);
@@ -455,7 +455,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_COUNT_FF, 0);
-  k_count_ff<<<(ntasks + 255) / 256, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits,
+  k_count_ff<<<(ntasks + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits,
                                                           c->d_chunk_off, c->d_frame_bits,
                                                           c->d_chunk_ff, g.nchunks, ntasks);
   tmark(c, MJG_K_COUNT_FF, 1);

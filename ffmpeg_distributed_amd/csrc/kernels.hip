@@ -561,24 +561,26 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
-// Thread per chunk: realign the chunk's words to its frame offset and count the 0xFF
-// bytes among the bytes it owns (a byte belongs to the chunk holding its first bit).
+// Wave per chunk (4 per workgroup), lane = word: realign the chunk's words to its frame
+// offset and count the 0xFF bytes among the bytes it owns (a byte belongs to the chunk
+// holding its first bit).
 __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
                                                   const uint32_t *__restrict__ chunk_bits,
                                                   const uint32_t *__restrict__ chunk_off,
                                                   const uint32_t *__restrict__ frame_bits,
                                                   uint32_t *__restrict__ chunk_ff, int nchunks,
                                                   int ntotal) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= ntotal) return;
   const int f = i / nchunks, c = i - f * nchunks;
   const uint32_t O = chunk_off[i], L = chunk_bits[i], T = frame_bits[f];
   const uint32_t total_bytes = (T + 7) >> 3;
   const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-  uint32_t cnt = 0;
-  for (uint32_t k = k0; k < k1; k++)
+  int cnt = 0;
+  for (uint32_t k = k0 + lane; k < k1; k += 64)
     cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k), 4 * k, total_bytes);
-  chunk_ff[i] = cnt;
+  cnt = wave_sum(cnt);
+  if (lane == 0) chunk_ff[i] = (uint32_t)cnt;
 }
 
 __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ chunk_ff,
@@ -621,15 +623,16 @@ __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ f
   }
 }
 
-// Thread per chunk: the chunk's owned bytes, a 0x00 after every 0xFF
-// (ff_mjpeg_escape_FF), at header + unstuffed position + 0xFFs before it in the frame.
+// Wave per chunk, lane = word: the chunk's owned bytes with a 0x00 after every 0xFF
+// (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs before it in the
+// frame (chunk prefix from k_scan_ff, in-chunk prefix by a wave scan).
 __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
     const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
     const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
     const uint64_t *__restrict__ frame_offsets, int hdr_len, int nchunks, int ntotal,
     uint8_t *__restrict__ out, uint64_t out_cap) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= ntotal) return;
   const int f = i / nchunks, c = i - f * nchunks;
   const uint64_t foff = frame_offsets[f];
@@ -637,17 +640,28 @@ __global__ __launch_bounds__(256) void k_write(
   const uint32_t O = chunk_off[i], L = chunk_bits[i], T = frame_bits[f];
   const uint32_t total_bytes = (T + 7) >> 3;
   const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-  uint8_t *p = out + foff + hdr_len + 4 * (size_t)k0 + ff_off[i];
-  for (uint32_t k = k0; k < k1; k++) {
-    const uint32_t v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
+  uint8_t *base = out + foff + hdr_len + 4 * (size_t)k0 + ff_off[i];
+  uint32_t carry = 0;
+  for (uint32_t kb = k0; kb < k1; kb += 64) {
+    const uint32_t k = kb + lane;
+    uint32_t v = 0, cnt = 0;
+    if (k < k1) {
+      v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
+      cnt = (uint32_t)ff_in_word(v, 4 * k, total_bytes);
+    }
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    if (k < k1) {
+      uint8_t *p = base + 4 * (k - k0) + carry + incl - cnt;
 #pragma unroll
-    for (int bb = 0; bb < 4; bb++) {
-      if (4 * k + bb < total_bytes) {
-        const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
-        *p++ = byte;
-        if (byte == 0xff) *p++ = 0;
+      for (int bb = 0; bb < 4; bb++) {
+        if (4 * k + bb < total_bytes) {
+          const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
+          *p++ = byte;
+          if (byte == 0xff) *p++ = 0;
+        }
       }
     }
+    carry += __shfl(incl, 63, 64);
   }
 }
 
