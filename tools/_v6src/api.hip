@@ -1,0 +1,632 @@
+// C-ABI of libmjgpu.so (declarations and boundary citations: include/mjgpu.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mjgpu.h"
+#include "jpeg_tables.h"
+#include "kernels.hip"
+#include "scale.hip"
+#include "sws_filter.h"
+
+using namespace mjg;
+
+namespace {
+
+thread_local std::string g_err = "no error";
+
+int set_err(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return set_err(MJG_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+// JPEG header of the profile: mjpegenc_common.c ff_mjpeg_encode_picture_header for
+// AV_CODEC_ID_MJPEG 4:2:0, -bitexact (no COM), equal luma/chroma matrices (one DQT),
+// frame threading (no DRI), -huffman default (one DHT with DC0, DC1, AC0, AC1).
+struct ByteWriter {
+  std::vector<uint8_t> b;
+  void u8(int v) { b.push_back((uint8_t)v); }
+  void u16(int v) { u8(v >> 8); u8(v); }
+};
+
+std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sar_num, int sar_den) {
+  ByteWriter o;
+  o.u16(0xFFD8);
+  if (sar_num > 0 && sar_den > 0) {
+    o.u16(0xFFE0);
+    o.u16(16);
+    for (char c : {'J', 'F', 'I', 'F', '\0'}) o.u8(c);
+    o.u16(0x0102);
+    o.u8(0);
+    o.u16(sar_num);
+    o.u16(sar_den);
+    o.u8(0);
+    o.u8(0);
+  }
+  o.u16(0xFFDB);
+  o.u16(2 + 65);
+  o.u8(0x00);
+  for (int i = 0; i < 64; i++) o.u8(mprime[kZigzag[i]]);
+  o.u16(0xFFC4);
+  const size_t len_at = o.b.size();
+  o.u16(0);
+  auto table = [&](int cls_id, const uint8_t *bits, const uint8_t *vals) {
+    o.u8(cls_id);
+    int n = 0;
+    for (int i = 1; i <= 16; i++) {
+      o.u8(bits[i]);
+      n += bits[i];
+    }
+    for (int i = 0; i < n; i++) o.u8(vals[i]);
+  };
+  table(0x00, kBitsDcLum, kValDc);
+  table(0x01, kBitsDcChr, kValDc);
+  table(0x10, kBitsAcLum, kValAcLum);
+  table(0x11, kBitsAcChr, kValAcChr);
+  const size_t dht_len = o.b.size() - len_at;
+  o.b[len_at] = (uint8_t)(dht_len >> 8);
+  o.b[len_at + 1] = (uint8_t)dht_len;
+  o.u16(0xFFC0);
+  o.u16(17);
+  o.u8(8);
+  o.u16(h);
+  o.u16(w);
+  o.u8(3);
+  o.u8(1); o.u8(0x22); o.u8(0);
+  o.u8(2); o.u8(0x11); o.u8(0);
+  o.u8(3); o.u8(0x11); o.u8(0);
+  o.u16(0xFFDA);
+  o.u16(12);
+  o.u8(3);
+  o.u8(1); o.u8(0x00);
+  o.u8(2); o.u8(0x11);
+  o.u8(3); o.u8(0x11);
+  o.u8(0); o.u8(63); o.u8(0);
+  return o.b;
+}
+
+template <typename T>
+int dmalloc(T **p, size_t count) {
+  *p = nullptr;
+  if (count == 0) return MJG_OK;
+  if (hipMalloc((void **)p, count * sizeof(T)) != hipSuccess) {
+    *p = nullptr;
+    (void)hipGetLastError();
+    return set_err(MJG_E_NOMEM, "hipMalloc(%zu bytes) failed", count * sizeof(T));
+  }
+  return MJG_OK;
+}
+
+struct PlaneScale {
+  SwsFilter hf, vf;
+  int16_t *hc = nullptr, *vc = nullptr;
+  int32_t *hp = nullptr, *vp = nullptr;
+  ScaleGeom g{};
+  size_t lds = 0;
+  dim3 grid;
+};
+
+}  // namespace
+
+struct mjg_ctx {
+  int device = 0;
+  mjg_config cfg{};
+  hipStream_t stream = nullptr;
+  EncGeom geom{};
+  int32_t qmat[64];
+  int enc_grid = 0;
+  bool scale = false;
+  size_t in_frame_bytes = 0, enc_frame_bytes = 0;
+  std::vector<uint8_t> hdr;
+  uint8_t mprime[64];
+
+  uint32_t *d_tabs = nullptr;
+  uint8_t *d_hdr = nullptr;
+  uint8_t *d_stage = nullptr, *d_scaled = nullptr;
+  uint32_t *d_scratch = nullptr;
+  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_chunk_ff = nullptr, *d_ff_off = nullptr;
+  uint32_t *d_frame_bits = nullptr, *d_status = nullptr;
+  uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
+  uint8_t *d_out = nullptr;
+  size_t out_cap = 0;
+  int16_t *d_dbg = nullptr;
+  PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
+
+  uint64_t *h_sizes = nullptr;
+  uint32_t *h_status = nullptr;
+  int last_n = 0;
+  bool pending = false, synced = false;
+  uint64_t last_total = 0;
+
+  bool timing = false;
+  hipEvent_t ev[MJG_NUM_KERNELS][2];
+  double t_acc[MJG_NUM_KERNELS] = {0};
+  int t_n = 0;
+};
+
+namespace {
+
+void free_ctx(mjg_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
+                  c->d_chunk_off, c->d_chunk_ff, c->d_ff_off, c->d_frame_bits, c->d_status,
+                  c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->ps[0].hc,
+                  c->ps[0].vc, c->ps[0].hp, c->ps[0].vp, c->ps[1].hc, c->ps[1].vc, c->ps[1].hp,
+                  c->ps[1].vp};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->h_sizes) (void)hipHostFree(c->h_sizes);
+  if (c->h_status) (void)hipHostFree(c->h_status);
+  if (c->timing)
+    for (auto &e : c->ev) {
+      (void)hipEventDestroy(e[0]);
+      (void)hipEventDestroy(e[1]);
+    }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh, int chroma,
+                      bool bitexact) {
+  const int pos = chroma ? sws_local_pos(1, -513) : sws_local_pos(0, 0);
+  if (!make_sws_filter(sw, dw, 1 << 14, 4, bitexact, pos, pos, &p.hf) ||
+      !make_sws_filter(sh, dh, 1 << 12, 2, bitexact, pos, pos, &p.vf))
+    return set_err(MJG_E_INVALID, "scale %dx%d -> %dx%d needs swscale's cascade (unsupported)", sw,
+                   sh, dw, dh);
+  // LDS extents over all tiles (positions are monotone after initFilter's reduce step).
+  int max_rows = 0, max_cols = 0;
+  for (int y0 = 0; y0 < dh; y0 += kScaleTileH) {
+    const int ye = std::min(y0 + kScaleTileH, dh);
+    max_rows = std::max(max_rows, p.vf.pos[ye - 1] + p.vf.taps - p.vf.pos[y0]);
+  }
+  for (int x0 = 0; x0 < dw; x0 += kScaleTileW) {
+    const int xe = std::min(x0 + kScaleTileW, dw);
+    max_cols = std::max(max_cols, p.hf.pos[xe - 1] + p.hf.taps - p.hf.pos[x0]);
+  }
+  for (int i = 1; i < dw; i++)
+    if (p.hf.pos[i] < p.hf.pos[i - 1]) return set_err(MJG_E_INVALID, "non-monotone hscale");
+  for (int i = 1; i < dh; i++)
+    if (p.vf.pos[i] < p.vf.pos[i - 1]) return set_err(MJG_E_INVALID, "non-monotone vscale");
+  ScaleGeom &g = p.g;
+  g.htaps = p.hf.taps;
+  g.vtaps = p.vf.taps;
+  g.lds_cols = (max_cols + 15) & ~15;
+  g.lds_rows = max_rows;
+  p.lds = (size_t)g.lds_rows * g.lds_cols + (size_t)g.lds_rows * kScaleTileW * 2;
+  if (p.lds > 64 * 1024)
+    return set_err(MJG_E_INVALID, "scale ratio too large for one LDS tile (%zu B)", p.lds);
+  p.grid = dim3((dw + kScaleTileW - 1) / kScaleTileW, (dh + kScaleTileH - 1) / kScaleTileH, 1);
+  int rc;
+  if ((rc = dmalloc(&p.hc, p.hf.coeff.size())) || (rc = dmalloc(&p.hp, p.hf.pos.size())) ||
+      (rc = dmalloc(&p.vc, p.vf.coeff.size())) || (rc = dmalloc(&p.vp, p.vf.pos.size())))
+    return rc;
+  HIP_TRY(hipMemcpy(p.hc, p.hf.coeff.data(), p.hf.coeff.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.hp, p.hf.pos.data(), p.hf.pos.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.vc, p.vf.coeff.data(), p.vf.coeff.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.vp, p.vf.pos.data(), p.vf.pos.size() * 4, hipMemcpyHostToDevice));
+  (void)c;
+  return MJG_OK;
+}
+
+int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
+  c->device = device;
+  c->cfg = *cfg;
+  const mjg_config &k = *cfg;
+  if (k.src_w < 1 || k.src_h < 1 || k.dst_w < 1 || k.dst_h < 1 || k.src_w > 16384 ||
+      k.src_h > 16384 || k.dst_w > 16384 || k.dst_h > 16384)
+    return set_err(MJG_E_INVALID, "bad frame size %dx%d -> %dx%d", k.src_w, k.src_h, k.dst_w, k.dst_h);
+  if (k.qscale < 1 || k.qscale > 31) return set_err(MJG_E_INVALID, "qscale %d not in 1..31", k.qscale);
+  if (k.max_batch < 1 || k.max_batch > 65535)
+    return set_err(MJG_E_INVALID, "max_batch %d not in 1..65535", k.max_batch);
+  if (k.sar_num < 0 || k.sar_den < 0 || k.sar_num > 65535 || k.sar_den > 65535)
+    return set_err(MJG_E_INVALID, "bad SAR %d:%d", k.sar_num, k.sar_den);
+
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return set_err(MJG_E_INVALID, "device %d of %d", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+
+  c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
+  const int scw = (k.src_w + 1) >> 1, sch = (k.src_h + 1) >> 1;
+  const int w = k.dst_w, h = k.dst_h, cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+  c->in_frame_bytes = (size_t)k.src_w * k.src_h + 2 * (size_t)scw * sch;
+  c->enc_frame_bytes = (size_t)w * h + 2 * (size_t)cw * ch;
+
+  EncGeom &g = c->geom;
+  g.w = w;
+  g.h = h;
+  g.cw = cw;
+  g.ch = ch;
+  g.mbw = (w + 15) / 16;
+  g.nmcu = g.mbw * ((h + 15) / 16);
+  g.nchunks = (g.nmcu * 6 + 63) / 64;  // chunks of 64 blocks (one wave each)
+  g.y_stride = w;
+  g.c_stride = cw;
+  g.u_off = (long long)w * h;
+  g.v_off = g.u_off + (long long)cw * ch;
+  g.frame_stride = (long long)c->enc_frame_bytes;
+  g.range_convert = (!c->scale && !k.in_full_range) ? 1 : 0;
+  g.debug_coefs = (k.flags & MJG_F_DEBUG_COEFS) ? 1 : 0;
+
+  // mpegvideo_enc.c encode_picture FMT_MJPEG matrix + ff_convert_matrix (qscale -> 8).
+  for (int i = 0; i < 64; i++) {
+    int v = i == 0 ? 8 : ((kMpeg1Intra[i] * k.qscale) >> 3);
+    v = v > 255 ? 255 : v;
+    c->mprime[i] = (uint8_t)v;
+    c->qmat[i] = (int32_t)((2ull << 21) / (uint64_t)(16 * v));
+  }
+  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den);
+
+  // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
+  // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row])
+  uint32_t tabs[608] = {0};
+  build_huffman(tabs, kBitsAcLum, kValAcLum);
+  build_huffman(tabs + 256, kBitsAcChr, kValAcChr);
+  uint32_t dc[256];
+  build_huffman(dc, kBitsDcLum, kValDc);
+  for (int i = 0; i < 16; i++) tabs[512 + i] = dc[i];
+  build_huffman(dc, kBitsDcChr, kValDc);
+  for (int i = 0; i < 16; i++) tabs[528 + i] = dc[i];
+  for (int i = 0; i < 64; i++) tabs[544 + (i & 7) * 8 + (i >> 3)] = (uint32_t)c->qmat[i];  // [col][row]
+
+  const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks;
+  int rc;
+  if ((rc = dmalloc(&c->d_tabs, 608)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
+      (rc = dmalloc(&c->d_scratch, B * NC * (size_t)kSlotWords)) ||
+      (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
+      (rc = dmalloc(&c->d_chunk_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
+      (rc = dmalloc(&c->d_frame_bits, B)) || (rc = dmalloc(&c->d_status, 4)) ||
+      (rc = dmalloc(&c->d_frame_size, B)) || (rc = dmalloc(&c->d_frame_offsets, B + 1)))
+    return rc;
+  c->out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096);
+  if ((rc = dmalloc(&c->d_out, c->out_cap))) return rc;
+  if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
+  if (g.debug_coefs && (rc = dmalloc(&c->d_dbg, B * (size_t)g.nmcu * 6 * 64))) return rc;
+  HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipHostMalloc((void **)&c->h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void **)&c->h_status, 16, hipHostMallocDefault));
+
+  if (c->scale) {
+    const bool bitexact = !(k.flags & MJG_F_SWS_NO_BITEXACT);
+    if ((rc = setup_plane_scale(c, c->ps[0], k.src_w, k.src_h, w, h, 0, bitexact)) ||
+        (rc = setup_plane_scale(c, c->ps[1], scw, sch, cw, ch, 1, bitexact)))
+      return rc;
+    for (int p = 0; p < 2; p++) {
+      ScaleGeom &sg = c->ps[p].g;
+      sg.sw = p ? scw : k.src_w;
+      sg.sh = p ? sch : k.src_h;
+      sg.dw = p ? cw : w;
+      sg.dh = p ? ch : h;
+      sg.s_stride = sg.sw;
+      sg.d_stride = sg.dw;
+      sg.s_fstride = (long long)c->in_frame_bytes;
+      sg.d_fstride = (long long)c->enc_frame_bytes;
+      sg.range = k.in_full_range ? 0 : (p ? 2 : 1);
+    }
+  }
+
+  // persistent k_encode grid: every CU filled with as many workgroups as fit
+  int ncu = 0, per_cu = 0;
+  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode, 64 * kWavesPerWg, 0));
+  c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
+
+  c->timing = (k.flags & MJG_F_TIMING) != 0;
+  if (c->timing)
+    for (auto &e : c->ev) {
+      HIP_TRY(hipEventCreate(&e[0]));
+      HIP_TRY(hipEventCreate(&e[1]));
+    }
+  return MJG_OK;
+}
+
+void tmark(mjg_ctx *c, int k, int end) {
+  if (c->timing) (void)hipEventRecord(c->ev[k][end], c->stream);
+}
+
+int launch_write(mjg_ctx *c, int n) {
+  const EncGeom &g = c->geom;
+  const int ntasks = g.nchunks * n;
+  HIP_TRY(hipMemsetAsync(c->d_status, 0, 4, c->stream));
+  tmark(c, MJG_K_WRITE, 0);
+  k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
+                                       (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status);
+  k_write<<<(ntasks + 3) / 4, 256, 0, c->stream>>>(
+      c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
+      c->d_frame_offsets, (int)c->hdr.size(), g.nchunks, ntasks, c->d_out, (uint64_t)c->out_cap);
+  tmark(c, MJG_K_WRITE, 1);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(c->h_sizes, c->d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, c->stream));
+  return MJG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mjg_version(void) { return 100; }
+
+const char *mjg_last_error(void) { return g_err.c_str(); }
+
+int mjg_device_count(void) {
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  return n;
+}
+
+int mjg_open(int device, const mjg_config *cfg, mjg_ctx **out) {
+  if (!cfg || !out) return set_err(MJG_E_INVALID, "null argument");
+  *out = nullptr;
+  mjg_ctx *c = new mjg_ctx();
+  const int rc = open_ctx(device, cfg, c);
+  if (rc) {
+    const std::string keep = g_err;
+    free_ctx(c);
+    g_err = keep;
+    return rc;
+  }
+  *out = c;
+  return MJG_OK;
+}
+
+void mjg_close(mjg_ctx *ctx) { free_ctx(ctx); }
+
+size_t mjg_frame_bytes(const mjg_ctx *ctx) { return ctx ? ctx->in_frame_bytes : 0; }
+
+int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len) {
+  if (!ctx) return set_err(MJG_E_INVALID, "null ctx");
+  if (len) *len = ctx->hdr.size();
+  if (!out) return MJG_OK;
+  if (cap < ctx->hdr.size()) return set_err(MJG_E_CAPACITY, "header needs %zu bytes", ctx->hdr.size());
+  memcpy(out, ctx->hdr.data(), ctx->hdr.size());
+  return MJG_OK;
+}
+
+int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
+  if (!c || !frames) return set_err(MJG_E_INVALID, "null argument");
+  if (n < 1 || n > c->cfg.max_batch)
+    return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
+  if (c->pending) return set_err(MJG_E_STATE, "previous submit not synced");
+  HIP_TRY(hipSetDevice(c->device));
+  const EncGeom &g = c->geom;
+  const uint8_t *src = frames;
+  if (!src_is_device) {
+    if (!c->d_stage) {  // staging for host submits, allocated on first use
+      const int rc = dmalloc(&c->d_stage, (size_t)c->cfg.max_batch * c->in_frame_bytes);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_stage, frames, (size_t)n * c->in_frame_bytes, hipMemcpyHostToDevice,
+                           c->stream));
+    src = c->d_stage;
+  }
+  const uint8_t *enc_in = src;
+  if (c->scale) {
+    tmark(c, MJG_K_SCALE, 0);
+    const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
+    for (int p = 0; p < 3; p++) {
+      PlaneScale &ps = c->ps[p ? 1 : 0];
+      ScaleGeom sg = p ? cg : lg;
+      if (p) {
+        sg.s_off = (long long)c->cfg.src_w * c->cfg.src_h + (p - 1) * (long long)cg.sw * cg.sh;
+        sg.d_off = g.u_off + (p - 1) * (long long)g.cw * g.ch;
+      } else {
+        sg.s_off = 0;
+        sg.d_off = 0;
+      }
+      dim3 grid = ps.grid;
+      grid.z = n;
+      k_scale<<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hc, ps.hp, ps.vc, ps.vp);
+    }
+    tmark(c, MJG_K_SCALE, 1);
+    HIP_TRY(hipGetLastError());
+    enc_in = c->d_scaled;
+  }
+  tmark(c, MJG_K_ENCODE, 0);
+  const int ntasks = g.nchunks * n;
+  const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
+  k_encode<<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
+                                                    c->d_chunk_bits, c->d_dbg, ntasks);
+  tmark(c, MJG_K_ENCODE, 1);
+  HIP_TRY(hipGetLastError());
+  tmark(c, MJG_K_SCAN_BITS, 0);
+  k_scan_bits<<<n, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, g.nchunks);
+  tmark(c, MJG_K_SCAN_BITS, 1);
+  HIP_TRY(hipGetLastError());
+  tmark(c, MJG_K_COUNT_FF, 0);
+  k_count_ff<<<(ntasks + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits,
+                                                          c->d_chunk_off, c->d_frame_bits,
+                                                          c->d_chunk_ff, g.nchunks, ntasks);
+  tmark(c, MJG_K_COUNT_FF, 1);
+  HIP_TRY(hipGetLastError());
+  tmark(c, MJG_K_SCAN_FF, 0);
+  k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_chunk_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
+                                       g.nchunks, (int)c->hdr.size());
+  tmark(c, MJG_K_SCAN_FF, 1);
+  HIP_TRY(hipGetLastError());
+  int rc = launch_write(c, n);
+  if (rc) return rc;
+  c->last_n = n;
+  c->pending = true;
+  c->synced = false;
+  return MJG_OK;
+}
+
+int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
+  if (!c) return set_err(MJG_E_INVALID, "null ctx");
+  if (!c->pending && !c->synced) return set_err(MJG_E_STATE, "nothing submitted");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->pending) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int n = c->last_n;
+    uint64_t t = 0;
+    for (int i = 0; i < n; i++) t += c->h_sizes[i];
+    if (*c->h_status & 1u) {  // packed output overflowed: grow, re-run the write pass only
+      HIP_TRY(hipFree(c->d_out));
+      c->d_out = nullptr;
+      c->out_cap = t + t / 4 + 4096;
+      int rc = dmalloc(&c->d_out, c->out_cap);
+      if (rc) return rc;
+      if ((rc = launch_write(c, n))) return rc;
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (*c->h_status & 1u) return set_err(MJG_E_HIP, "output overflow persisted");
+    }
+    if (c->timing) {
+      for (int k = 0; k < MJG_NUM_KERNELS; k++) {
+        if (k == MJG_K_SCALE && !c->scale) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->ev[k][0], c->ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
+      }
+      c->t_n++;
+    }
+    c->last_total = t;
+    c->pending = false;
+    c->synced = true;
+  }
+  if (frame_sizes) memcpy(frame_sizes, c->h_sizes, c->last_n * sizeof(uint64_t));
+  if (total) *total = c->last_total;
+  return MJG_OK;
+}
+
+int mjg_fetch(mjg_ctx *c, uint8_t *out, size_t cap) {
+  if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
+  int rc = mjg_sync(c, nullptr, nullptr);
+  if (rc) return rc;
+  if (cap < c->last_total) return set_err(MJG_E_CAPACITY, "fetch needs %llu bytes",
+                                          (unsigned long long)c->last_total);
+  HIP_TRY(hipMemcpyAsync(out, c->d_out, c->last_total, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MJG_OK;
+}
+
+int mjg_output_device(mjg_ctx *c, const uint8_t **data, const uint64_t **offsets) {
+  if (!c) return set_err(MJG_E_INVALID, "null ctx");
+  if (data) *data = c->d_out;
+  if (offsets) *offsets = c->d_frame_offsets;
+  return MJG_OK;
+}
+
+void *mjg_stream(mjg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int mjg_host_alloc(size_t bytes, void **ptr) {
+  if (!ptr) return set_err(MJG_E_INVALID, "null argument");
+  if (hipHostMalloc(ptr, bytes, hipHostMallocDefault) != hipSuccess) {
+    *ptr = nullptr;
+    (void)hipGetLastError();
+    return set_err(MJG_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+  }
+  return MJG_OK;
+}
+
+int mjg_host_free(void *ptr) {
+  if (ptr) HIP_TRY(hipHostFree(ptr));
+  return MJG_OK;
+}
+
+int mjg_kernel_times(mjg_ctx *c, double *ms, int *launches, int reset) {
+  if (!c) return set_err(MJG_E_INVALID, "null ctx");
+  if (!c->timing) return set_err(MJG_E_STATE, "context opened without MJG_F_TIMING");
+  for (int k = 0; k < MJG_NUM_KERNELS; k++)
+    if (ms) ms[k] = c->t_n ? c->t_acc[k] / c->t_n : 0.0;
+  if (launches) *launches = c->t_n;
+  if (reset) {
+    for (double &t : c->t_acc) t = 0;
+    c->t_n = 0;
+  }
+  return MJG_OK;
+}
+
+int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *len) {
+  if (!cfg) return set_err(MJG_E_INVALID, "null cfg");
+  if (cfg->dst_w < 1 || cfg->dst_h < 1 || cfg->dst_w > 65535 || cfg->dst_h > 65535 ||
+      cfg->qscale < 1 || cfg->qscale > 31)
+    return set_err(MJG_E_INVALID, "bad size / qscale");
+  uint8_t mp[64];
+  for (int i = 0; i < 64; i++) {
+    const int v = i == 0 ? 8 : ((kMpeg1Intra[i] * cfg->qscale) >> 3);
+    mp[i] = (uint8_t)(v > 255 ? 255 : v);
+  }
+  const std::vector<uint8_t> h = build_header(cfg->dst_w, cfg->dst_h, mp, cfg->sar_num, cfg->sar_den);
+  if (len) *len = h.size();
+  if (!out) return MJG_OK;
+  if (cap < h.size()) return set_err(MJG_E_CAPACITY, "header needs %zu bytes", h.size());
+  memcpy(out, h.data(), h.size());
+  return MJG_OK;
+}
+
+int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, int src_pos,
+                   int dst_pos, int16_t *coeff, size_t coeff_cap, int32_t *pos_out, int *taps) {
+  SwsFilter f;
+  if (!make_sws_filter(src_len, dst_len, one, align, bitexact != 0, src_pos, dst_pos, &f))
+    return set_err(MJG_E_INVALID, "unsupported filter %d -> %d", src_len, dst_len);
+  if (taps) *taps = f.taps;
+  if (!coeff) return MJG_OK;
+  if (coeff_cap < f.coeff.size()) return set_err(MJG_E_CAPACITY, "need %zu taps", f.coeff.size());
+  memcpy(coeff, f.coeff.data(), f.coeff.size() * sizeof(int16_t));
+  if (pos_out) memcpy(pos_out, f.pos.data(), f.pos.size() * sizeof(int32_t));
+  return MJG_OK;
+}
+
+int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
+  if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
+  if (!c->d_dbg) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
+  int rc = mjg_sync(c, nullptr, nullptr);
+  if (rc) return rc;
+  const size_t nb = (size_t)c->geom.nmcu * 6;  // dbg buffer: frame-major, block order
+  if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
+  if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
+  std::vector<int16_t> zz(nb * 64);  // kernel stores zigzag order
+  HIP_TRY(hipMemcpy(zz.data(), c->d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
+                    hipMemcpyDeviceToHost));
+  for (size_t b = 0; b < nb; b++)
+    for (int k = 0; k < 64; k++) out[b * 64 + kZigzag[k]] = zz[b * 64 + k];
+  return MJG_OK;
+}
+
+int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
+  if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
+  if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale");
+  int rc = mjg_sync(c, nullptr, nullptr);
+  if (rc) return rc;
+  if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
+  if (cap < c->enc_frame_bytes) return set_err(MJG_E_CAPACITY, "need %zu bytes", c->enc_frame_bytes);
+  HIP_TRY(hipMemcpy(out, c->d_scaled + (size_t)frame * c->enc_frame_bytes, c->enc_frame_bytes,
+                    hipMemcpyDeviceToHost));
+  return MJG_OK;
+}
+
+int mjg_debug_filter(mjg_ctx *c, int plane, int dir, int16_t *coeff, int32_t *pos, int *taps,
+                     int *len) {
+  if (!c) return set_err(MJG_E_INVALID, "null ctx");
+  if (!c->scale) return set_err(MJG_E_STATE, "context does not scale");
+  if (plane < 0 || plane > 1 || dir < 0 || dir > 1) return set_err(MJG_E_INVALID, "plane/dir");
+  const SwsFilter &f = dir ? c->ps[plane].vf : c->ps[plane].hf;
+  if (taps) *taps = f.taps;
+  if (len) *len = f.dst_len;
+  if (coeff) memcpy(coeff, f.coeff.data(), f.coeff.size() * sizeof(int16_t));
+  if (pos) memcpy(pos, f.pos.data(), f.pos.size() * sizeof(int32_t));
+  return MJG_OK;
+}
+
+}  // extern "C"

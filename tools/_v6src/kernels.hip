@@ -21,9 +21,6 @@
 
 #include "jpeg_tables.h"
 
-#ifndef MJG_ENC_WAVES_PER_EU
-#define MJG_ENC_WAVES_PER_EU 4  // k_encode occupancy target (waves per SIMD); measured best
-#endif
 #ifndef MJG_ABLATE
 #define MJG_ABLATE 0  // perf experiments only: 1 = no bit-pack
 #endif
@@ -188,8 +185,8 @@ struct RegSink {
 // Bit-pack one block's Huffman codes, FFmpeg mjpegenc.c encode_block /
 // mjpegenc_common.c ff_mjpeg_encode_dc (ZRL 0xF0 per 16 zeros, EOB unless coef 63 != 0).
 // Walks only the nonzero coefficients (64-bit zigzag mask); coefficients come from the
-// wave's LDS block image s_pk[word][lane] (int16 pairs), conflict-free for any per-lane k.
-// (Mean nonzero AC per block is ~1.2 on testsrc2 4K q5, so the loop is short.)
+// workgroup's LDS block image s_pk[word][thread] (int16 pairs), conflict-free for any
+// per-lane k.
 template <int STRIDE, class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask, int diff,
                                            const uint32_t *ac, const uint32_t *dc, Sink &sink) {
@@ -268,7 +265,7 @@ __device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s
 // Persistent grid: wave w encodes chunks [w*T, (w+1)*T) in (frame, chunk) order and
 // prefetches the next chunk's pixel rows into registers while encoding the current one.
 constexpr int kWavesPerWg = 4;
-constexpr int kWaveWinWords = 256;  // per-wave bit-pack window (1 KiB); heavier chunks loop
+constexpr int kWaveWinWords = 512;  // per-wave bit-pack window (2 KiB); heavier chunks loop
 
 __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g, int frame, int b) {
   const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
@@ -293,7 +290,7 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
   return s;
 }
 
-__global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_encode(
+__global__ __launch_bounds__(64 * kWavesPerWg) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, int ntasks) {
@@ -347,51 +344,18 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const int blk = b - 6 * (b / 6);
     const int tab = blk < 4 ? 0 : 1;
     if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, b));
-#if MJG_ABLATE >= 8  // perf experiment: 9 = pixel loads only, 8 = loads + row pass
-    {
-      uint32_t acc = 0;
-#if MJG_ABLATE == 8
-      for (int r = 0; r < 8; r++) {
-        int cr[8];
-        for (int x = 0; x < 8; x++) cr[x] = (int)((raw[r] >> (8 * x)) & 255u);
-        fdct8<1, true>(cr);
-        for (int x = 0; x < 8; x++) acc += cr[x];
-      }
-#else
-      for (int r = 0; r < 8; r++) acc += (uint32_t)raw[r] ^ (uint32_t)(raw[r] >> 32);
-#endif
-      if (t + 1 < t1) {
-        if (++chunk == nck) {
-          chunk = 0;
-          frame++;
-        }
-        b = chunk * 64 + lane;
-        active = b < nblk;
-        fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
-      }
-      acc = wave_sum((int)acc);
-      // keep acc live but publish a valid (empty) chunk: later kernels index by these lengths
-      if (lane == 0) chunk_bits[t] = (acc == 0x9e3779b9u) ? 32u : 0u;
-      continue;
-    }
-#endif
-    // unpack + tv->pc + FDCT row pass, one row at a time; the row outputs (int16 in
-    // FFmpeg, and they fit) go to this wave's LDS block image as pairs [row*4+j][lane].
-    // Luma and chroma share one range formula: chroma's (p*596864 - 9027848) >> 19 ==
-    // (p*2387456 - 36111392) >> 21.
+    // unpack + tv->pc + FDCT row pass, one row at a time.  Luma and chroma share one
+    // formula: chroma's (p*596864 - 9027848) >> 19 == (p*2387456 - 36111392) >> 21.
     const int rmul = tab ? 2387456 : 2441856, radd = tab ? 36111392 : 38008785;
+    int c[64];
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-      int cr[8];
 #pragma unroll
       for (int x = 0; x < 8; x++) {
         const int p = (int)((raw[r] >> (8 * x)) & 255u);
-        cr[x] = !rc ? p : min(max((__mul24(p, rmul) - radd) >> 21, 0), 255);
+        c[r * 8 + x] = !rc ? p : min(max((__mul24(p, rmul) - radd) >> 21, 0), 255);
       }
-      fdct8<1, true>(cr);
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        s_pk[(r * 4 + j) * 64 + lane] = ((uint32_t)cr[2 * j] & 0xffffu) | ((uint32_t)cr[2 * j + 1] << 16);
+      fdct8<1, true>(c + r * 8);
       __builtin_amdgcn_sched_barrier(0);
     }
     // prefetch the next chunk while this one is encoded
@@ -407,64 +371,44 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
     }
 
-    // Column pass two columns at a time from the LDS row image, each coefficient
-    // quantised straight into a packed zigzag register image (qpk), which then replaces
-    // the consumed row image.  dct_quantize_c (intra, MJPEG): DC (c+32)/64; AC
-    // sign(c) * ((|c|*qmat + 3<<18) >> 21), folded into one signed multiply-add:
-    // (c*qmat + (c < 0 ? 2^21-1-(3<<18) : 3<<18)) >> 21.  clip_coeffs (+-1023) never
-    // fires: |AC| <= ~6710 for 8-bit input, so |q| <= 419 even at qscale 1.
     int dc = 0;
     uint32_t mlo = 0, mhi = 0;
     if (cur_active) {
-      uint32_t qpk[32];
+      // Column pass, each column quantised as soon as it is done (short live ranges):
+      // dct_quantize_c (intra, MJPEG): DC (c+32)/64; AC (|c|*qmat + 3<<18) >> 21 with the
+      // sign restored.  clip_coeffs (+-1023) never fires: |AC| <= ~6710 for 8-bit input,
+      // so |q| <= (6710 * 2^17 + 3<<18) >> 21 = 419 even at qscale 1.
+      uint16_t *pk16 = (uint16_t *)s_pk;
 #pragma unroll
-      for (int i = 0; i < 32; i++) qpk[i] = 0;
-#pragma unroll
-      for (int jp = 0; jp < 4; jp++) {
-        __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
-        int cc[2][8];
+      for (int col = 0; col < 8; col++) {
+        __builtin_amdgcn_sched_barrier(0);  // one column in flight at a time
+        fdct8<8, false>(c + col);
+        const int4 qa = *(const int4 *)(s_qc + col * 8), qb = *(const int4 *)(s_qc + col * 8 + 4);
+        const int qm[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-          const uint32_t w = s_pk[(r * 4 + jp) * 64 + lane];
-          cc[0][r] = (int)(int16_t)(w & 0xffffu);
-          cc[1][r] = (int)(int16_t)(w >> 16);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          __builtin_amdgcn_sched_barrier(0);  // one column at a time
-          const int col = 2 * jp + h;
-          fdct8<1, false>(cc[h]);
-          const int4 qa = *(const int4 *)(s_qc + col * 8), qb = *(const int4 *)(s_qc + col * 8 + 4);
-          const int qm[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-#pragma unroll
-          for (int r = 0; r < 8; r++) {
-            const int k = kZigzagInv[r * 8 + col];
-            const int x = cc[h][r];
-            int v;
-            if (k == 0) {
-              dc = (x + 32) >> 6;
-              v = dc;
-            } else {
-              v = (__mul24(x, qm[r]) + (x < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
-              const uint32_t nz = min((uint32_t)v, 1u);
-              if (k < 32)
-                mlo |= nz << k;
-              else
-                mhi |= nz << (k - 32);
-            }
-            if (k & 1)
-              qpk[k >> 1] |= (uint32_t)v << 16;
+          const int k = kZigzagInv[r * 8 + col];
+          const int x = c[r * 8 + col];
+          int v;
+          if (k == 0) {
+            dc = (x + 32) >> 6;
+            v = dc;
+          } else {
+            const int ax = x < 0 ? -x : x;
+            const int q = (int)(__umul24((uint32_t)ax, (uint32_t)qm[r]) + (3u << 18)) >> 21;
+            v = x < 0 ? -q : q;
+            if (k < 32)
+              mlo |= q ? (1u << k) : 0u;
             else
-              qpk[k >> 1] |= (uint32_t)v & 0xffffu;
+              mhi |= q ? (1u << (k - 32)) : 0u;
           }
+          pk16[((k >> 1) * 64 + lane) * 2 + (k & 1)] = (uint16_t)v;
         }
       }
-#pragma unroll
-      for (int i = 0; i < 32; i++) s_pk[i * 64 + lane] = qpk[i];
       if (g.debug_coefs) {  // packed zigzag pairs; the host reorders (mjg_debug_coefs)
         uint32_t *o = (uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64);
 #pragma unroll
-        for (int k = 0; k < 32; k++) o[k] = qpk[k];
+        for (int k = 0; k < 32; k++) o[k] = s_pk[k * 64 + lane];
       }
     }
     const uint64_t mask = ((uint64_t)mhi << 32) | mlo;
@@ -563,17 +507,12 @@ __device__ uint32_t block_excl_scan(const uint32_t *in, uint32_t *out, int n) {
   return s_carry;
 }
 
-// Per-frame exclusive scan of the chunk bit lengths.  Lengths are clamped to the slot
-// size first, so a corrupted length can never send the realign/stuff kernels outside
-// their slots (defence in depth; k_encode never writes more than a slot).
-__global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk_bits,
+__global__ __launch_bounds__(1024) void k_scan_bits(const uint32_t *__restrict__ chunk_bits,
                                                     uint32_t *__restrict__ chunk_off,
                                                     uint32_t *__restrict__ frame_bits, int nchunks) {
   const int f = blockIdx.x;
-  uint32_t *cb = chunk_bits + (size_t)f * nchunks;
-  for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
-  __syncthreads();
-  const uint32_t t = block_excl_scan(cb, chunk_off + (size_t)f * nchunks, nchunks);
+  const uint32_t t = block_excl_scan(chunk_bits + (size_t)f * nchunks, chunk_off + (size_t)f * nchunks,
+                                     nchunks);
   if (threadIdx.x == 0) frame_bits[f] = t;
 }
 

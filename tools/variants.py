@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Perf A/B of k_encode source variants in ONE process, interleaved rounds (guide §5.4
+rule 24).  VARIANTS="name=srcdir:flags;..." where srcdir holds api.hip & friends
+(default: the working tree) and flags are extra hipcc -D options.  Only kernel times
+are compared; run tests/test_gpu_parity.py for correctness of the shipped build."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+CSRC = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
+
+
+def parse():
+    out = []
+    for item in os.environ.get("VARIANTS", "cur=:").split(";"):
+        name, rest = item.split("=", 1)
+        src, _, flags = rest.partition(":")
+        out.append((name, os.path.abspath(os.path.join(ROOT, src)) if src else CSRC, flags.split()))
+    return out
+
+
+def build(name, src, flags):
+    so = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           *flags, "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(src, "api.hip"),
+           os.path.join(CSRC, "sws_filter.cpp")]
+    subprocess.run(cmd, check=True, cwd=src)
+    return so
+
+
+def main():
+    vs = parse()
+    if "--build" in sys.argv:
+        for v in vs:
+            build(*v)
+        return
+    import torch
+    from ffmpeg_distributed_amd import _lib
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    W, H, N = 3840, 2160, 120
+    dev = torch.device("cuda", 0)
+    pool = torch.empty((N, W * H * 3 // 2), dtype=torch.uint8, device=dev)
+    for i in range(0, N, 20):
+        pool[i:i + 20] = testsrc2_i420_torch(W, H, i, 20, dev)
+    torch.cuda.synchronize()
+    encs = {}
+    for name, _, _ in vs:
+        _lib._lib = None
+        _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
+        from ffmpeg_distributed_amd.encoder import MjpegEncoder
+        encs[name] = MjpegEncoder(0, W, H, qscale=5, max_batch=N, timing=True)
+    res = {n: [] for n in encs}
+    ref = None
+    for rnd in range(6):
+        for n, e in encs.items():
+            e.kernel_times(reset=True)
+            for _ in range(3):
+                e.submit(device_ptr=pool.data_ptr(), nframes=N)
+                sizes = e.sync()
+            if rnd == 0:
+                out = e.fetch()
+                ref = ref or out
+                print(f"{n}: output {'==' if out == ref else '!='} first variant", flush=True)
+            res[n].append(e.kernel_times()[0])
+    for n, rows in res.items():
+        enc = sorted(r["encode"] for r in rows)
+        tot = sorted(sum(r.values()) for r in rows)
+        print(f"{n:12s} k_encode median {enc[len(enc)//2]:.4f} ms (min {enc[0]:.4f}); "
+              f"all kernels median {tot[len(tot)//2]:.4f} ms per {N} frames")
+
+
+if __name__ == "__main__":
+    main()
