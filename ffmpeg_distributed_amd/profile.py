@@ -1,0 +1,179 @@
+"""Parse the reference's `remote_args` (ffmpeg_distributed.py:190 shlex-splits them and
+:134 passes them to the worker ffmpeg) into the GPU encode profile, or report why the
+arguments fall outside it (the worker then runs the real ffmpeg unchanged).
+
+Supported profile (BASELINE north star):
+    [-vf scale=W:H[:flags=bicubic...]] -c:v mjpeg -q:v N -dct int -huffman default -bitexact
+plus options that do not change the video bitstream: -an -sn -dn -y -threads N
+-pix_fmt yuvj420p -f matroska -map 0:v[:0].
+"""
+from __future__ import annotations
+
+import shlex
+from math import gcd
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple, Union
+
+
+@dataclass
+class Profile:
+    qscale: int                      # effective mpegvideo qscale (update_qscale mapping)
+    q_arg: float                     # the -q:v value as given
+    scale: Optional[Tuple[int, int]] = None   # -vf scale=W:H
+    sws_flags: Tuple[str, ...] = ("bicubic",)
+
+
+class Unsupported(ValueError):
+    pass
+
+
+def effective_qscale(q: float) -> int:
+    """mpegvideo_enc.c update_qscale for a fixed -q:v: lambda = q*FF_QP2LAMBDA(118),
+    qscale = (lambda*139 + 128*64) >> 14, clipped to [qmin=2, qmax=31]."""
+    lam = int(q * 118)
+    return max(2, min(31, (lam * 139 + 128 * 64) >> 14))
+
+
+_FLAGS_OK = {"bicubic", "accurate_rnd", "bitexact", "full_chroma_int", "full_chroma_inp"}
+
+
+def _parse_scale(vf: str) -> Tuple[Tuple[int, int], Tuple[str, ...]]:
+    if "," in vf or ";" in vf or not vf.startswith("scale="):
+        raise Unsupported(f"filter graph {vf!r} (only a single scale=W:H is GPU-accelerated)")
+    parts = vf[len("scale="):].split(":")
+    kv, pos = {}, []
+    for p in parts:
+        if "=" in p:
+            k, v = p.split("=", 1)
+            kv[k] = v
+        else:
+            pos.append(p)
+    w = kv.pop("w", kv.pop("width", pos[0] if len(pos) > 0 else None))
+    h = kv.pop("h", kv.pop("height", pos[1] if len(pos) > 1 else None))
+    flags = tuple(f for f in kv.pop("flags", "bicubic").replace("+", " ").split() if f)
+    if kv:
+        raise Unsupported(f"scale options {sorted(kv)}")
+    try:
+        W, H = int(w), int(h)
+    except (TypeError, ValueError):
+        raise Unsupported(f"scale size {w}:{h} (explicit positive W:H required)")
+    if W <= 0 or H <= 0:
+        raise Unsupported(f"scale size {W}:{H}")
+    if not flags or flags[0] != "bicubic" or any(f not in _FLAGS_OK for f in flags):
+        raise Unsupported(f"scale flags {flags}")
+    return (W, H), flags
+
+
+def parse(args: Union[str, Sequence[str]]) -> Profile:
+    """Profile for `remote_args`, or raise Unsupported(reason)."""
+    a: List[str] = shlex.split(args) if isinstance(args, str) else list(args)
+    codec = q = dct = huff = None
+    bitexact = False
+    scale = None
+    flags: Tuple[str, ...] = ("bicubic",)
+    i = 0
+
+    def val():
+        nonlocal i
+        if i + 1 >= len(a):
+            raise Unsupported(f"{a[i]} without a value")
+        i += 1
+        return a[i]
+
+    while i < len(a):
+        o = a[i]
+        if o in ("-c:v", "-codec:v", "-vcodec", "-c", "-codec"):
+            codec = val()
+        elif o in ("-q:v", "-qscale:v", "-q", "-qscale"):
+            try:
+                q = float(val())
+            except ValueError:
+                raise Unsupported(f"{o} {a[i]}")
+        elif o == "-dct":
+            dct = val()
+        elif o == "-huffman":
+            huff = val()
+        elif o == "-bitexact":
+            bitexact = True
+        elif o in ("-flags", "-flags:v", "-fflags"):
+            v = val()
+            if "+bitexact" in v or v == "bitexact":
+                bitexact = True
+            else:
+                raise Unsupported(f"{o} {v}")
+        elif o in ("-vf", "-filter:v"):
+            scale, flags = _parse_scale(val())
+        elif o in ("-an", "-sn", "-dn", "-y"):
+            pass
+        elif o == "-threads":
+            val()
+        elif o == "-pix_fmt":
+            if val() not in ("yuvj420p",):
+                raise Unsupported(f"-pix_fmt {a[i]} (GPU path writes 4:2:0 full range)")
+        elif o == "-f":
+            if val() != "matroska":
+                raise Unsupported(f"-f {a[i]}")
+        elif o == "-map":
+            if val() not in ("0:v", "0:v:0", "0"):
+                raise Unsupported(f"-map {a[i]}")
+        else:
+            raise Unsupported(f"option {o}")
+        i += 1
+    if codec != "mjpeg":
+        raise Unsupported(f"codec {codec!r}")
+    if q is None:
+        raise Unsupported("no -q:v (rate control modes are not GPU-accelerated)")
+    if dct != "int":
+        raise Unsupported(f"-dct {dct!r} (only the integer jfdctint is bit-exact reproducible)")
+    if huff != "default":
+        raise Unsupported(f"-huffman {huff!r} (optimal tables: next round)")
+    if not bitexact:
+        raise Unsupported("no -bitexact (the Lavc COM segment is build-specific)")
+    return Profile(qscale=effective_qscale(q), q_arg=q, scale=scale, sws_flags=flags)
+
+
+def av_reduce(num: int, den: int, max_v: int) -> Tuple[int, int]:
+    """libavutil av_reduce: the best rational approximation of num/den with both terms
+    <= max_v (continued-fraction convergents, then the best semiconvergent)."""
+    a0n, a0d, a1n, a1d = 0, 1, 1, 0
+    sign = (num < 0) != (den < 0)
+    num, den = abs(num), abs(den)
+    g = gcd(num, den)
+    if g:
+        num, den = num // g, den // g
+    if num <= max_v and den <= max_v:
+        a1n, a1d, den = num, den, 0
+    while den:
+        x = num // den
+        next_den = num - den * x
+        a2n, a2d = x * a1n + a0n, x * a1d + a0d
+        if a2n > max_v or a2d > max_v:
+            if a1n:
+                x = (max_v - a0n) // a1n
+            if a1d:
+                x = min(x, (max_v - a0d) // a1d)
+            if den * (2 * x * a1d + a0d) > num * a1d:
+                a1n, a1d = x * a1n + a0n, x * a1d + a0d
+            break
+        a0n, a0d, a1n, a1d = a1n, a1d, a2n, a2d
+        num, den = den, next_den
+    return (-a1n if sign else a1n), a1d
+
+
+def scaled_sar(sar: Tuple[int, int], src: Tuple[int, int], dst: Tuple[int, int]) -> Tuple[int, int]:
+    """Sample aspect ratio after the scale filter (vf_scale config_props: an unknown SAR
+    stays unknown, otherwise SAR * (out_h*in_w)/(out_w*in_h), reduced), then the 16-bit
+    reduction the JFIF APP0 writer applies (mjpegenc_common.c jpeg_put_comments)."""
+    if sar[0] <= 0 or sar[1] <= 0:
+        return (0, 0)
+    n, d = av_reduce(dst[1] * src[0] * sar[0], dst[0] * src[1] * sar[1], 2**31 - 1)
+    if n > 65535 or d > 65535:
+        n, d = av_reduce(n, d, 65535)
+    return n, d
+
+
+def try_parse(args) -> Tuple[Optional[Profile], Optional[str]]:
+    try:
+        return parse(args), None
+    except Unsupported as e:
+        return None, str(e)

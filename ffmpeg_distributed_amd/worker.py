@@ -1,0 +1,247 @@
+"""The `gpu:N` segment worker: the process the dispatcher starts in place of
+`nice -n10 ionice -c3 ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:`
+(ffmpeg_distributed.py:131-141), with the same contract: one segment on stdin, the
+encoded Matroska segment on stdout, ffmpeg-style `Duration:` / `frame= ... speed=Nx`
+lines on stderr (parsed at ffmpeg_distributed.py:39-40,62-73), exit code 0 on success.
+
+    python -m ffmpeg_distributed_amd.worker --device N <remote_args...>
+
+remote_args inside the GPU profile (profile.parse) are encoded on GPU N; anything else
+runs the reference command line with the real ffmpeg as a child (same output, CPU).
+
+Input: Matroska with V_UNCOMPRESSED I420 video and YUV4MPEG2 are read natively; any
+other codec (the splitter's lossless x264 segments, fd.py:198-202) is decoded by an
+`ffmpeg ... -f yuv4mpegpipe` child feeding this process (SURVEY §8f "splitter decode").
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import queue
+import subprocess
+import sys
+import threading
+import time
+from fractions import Fraction
+from typing import List, Optional
+
+from . import container, profile
+
+DECODE_ARGV = ["ffmpeg", "-v", "error", "-f", "matroska", "-i", "pipe:", "-map", "0:v:0",
+               "-f", "yuv4mpegpipe", "-strict", "-1", "pipe:"]
+BATCH = int(os.environ.get("MJG_WORKER_BATCH", "32"))
+
+
+def reference_argv(args: List[str]) -> List[str]:
+    """The command the reference runs for one segment (fd.py:133-135, without nice/ionice)."""
+    return ["ffmpeg", "-f", "matroska", "-i", "pipe:", *args, "-f", "matroska", "pipe:"]
+
+
+def _hms(t: float) -> str:
+    h, r = divmod(max(t, 0.0), 3600)
+    m, s = divmod(r, 60)
+    return f"{int(h):02d}:{int(m):02d}:{s:05.2f}"
+
+
+class Progress:
+    """ffmpeg-shaped stderr lines so FFMPEGProc's progress regex follows the GPU worker."""
+
+    def __init__(self, err, fps: Fraction, qscale: int):
+        self.err, self.fps, self.q = err, fps, qscale
+        self.t0 = time.monotonic()
+        self.last = 0.0
+        self.bytes = 0
+
+    def duration(self, seconds: Optional[float]):
+        if seconds is not None:
+            self.err.write(f"  Duration: {_hms(seconds)}, start: 0.000000, bitrate: N/A\n")
+            self.err.flush()
+
+    def update(self, frames: int, nbytes: int, final: bool = False):
+        self.bytes += nbytes
+        now = time.monotonic()
+        if not final and now - self.last < 0.5:
+            return
+        self.last = now
+        el = max(now - self.t0, 1e-6)
+        t = float(frames / self.fps) if self.fps else 0.0
+        kb = self.bytes // 1024
+        br = (self.bytes * 8 / t / 1000) if t > 0 else 0.0
+        self.err.write(f"frame={frames:5d} fps={int(frames / el):3d} q={self.q:.1f} "
+                       f"size={kb:8d}KiB time={_hms(t)} bitrate={br:7.1f}kbits/s "
+                       f"speed={t / el:.3f}x\n")
+        self.err.flush()
+
+
+class Source:
+    """Packed I420 frames from stdin: .info (StreamInfo), .read_into(buf, n) -> count."""
+
+    def __init__(self, raw):
+        self.child = None
+        self.feeder = None
+        head = raw.read(4)
+        if head.startswith(b"YUV4"):
+            self._y4m(container.Y4MReader(raw, head))
+            self.duration = None
+            return
+        if head != b"\x1a\x45\xdf\xa3":
+            raise ValueError("input is neither Matroska nor YUV4MPEG2")
+        mkv = container.MkvReader(raw, head, record=True)
+        tr = next((t for t in mkv.tracks if t.codec.startswith("V_")), None)
+        if tr is None:
+            raise ValueError("no video track in the segment")
+        self.duration = mkv.duration_seconds()
+        info = mkv.info(tr.number)
+        if tr.codec == "V_UNCOMPRESSED" and tr.colour_space in (b"I420", b""):
+            self.info = info
+            self._frames = mkv.frames(tr.number)
+            self.read_into = self._read_mkv
+            return
+        # any other codec: ffmpeg decodes, we read its y4m
+        self.child = subprocess.Popen(DECODE_ARGV, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+        self.feeder = threading.Thread(target=self._feed, args=(mkv, raw), daemon=True)
+        self.feeder.start()
+        self._y4m(container.Y4MReader(self.child.stdout))
+
+    def _feed(self, mkv, raw):
+        # the decoder gets the exact bytes we consumed: replay them, then the rest
+        try:
+            self.child.stdin.write(mkv.replay_bytes())
+            while True:
+                b = raw.read(1 << 20)
+                if not b:
+                    break
+                self.child.stdin.write(b)
+        except BrokenPipeError:
+            pass
+        finally:
+            try:
+                self.child.stdin.close()
+            except BrokenPipeError:
+                pass
+
+    def _y4m(self, rd):
+        self.info = rd.info
+        self.read_into = rd.read_into
+
+    def _read_mkv(self, buf, n):
+        fb = self.info.frame_bytes
+        mv = memoryview(buf).cast("B")
+        for i in range(n):
+            try:
+                _, data = next(self._frames)
+            except StopIteration:
+                return i
+            if len(data) != fb:
+                raise ValueError(f"V_UNCOMPRESSED frame of {len(data)} bytes, expected I420 {fb}")
+            mv[i * fb:(i + 1) * fb] = data
+        return n
+
+    def close(self) -> int:
+        if self.child is None:
+            return 0
+        self.child.stdout.close()
+        return self.child.wait()
+
+
+def passthrough(args: List[str]) -> int:
+    """Outside the GPU profile: run exactly what the reference runs."""
+    try:
+        return subprocess.call(reference_argv(args))
+    except FileNotFoundError:
+        sys.stderr.write("ffmpeg not found for a non-GPU profile\n")
+        return 127
+
+
+def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> int:
+    stdin = stdin or sys.stdin.buffer
+    stdout = stdout or sys.stdout.buffer
+    stderr = stderr or sys.stderr
+    prof, why = profile.try_parse(args)
+    if prof is None:
+        stderr.write(f"gpu:{device}: {why}; running ffmpeg on the CPU\n")
+        stderr.flush()
+        return passthrough(args)
+
+    src = Source(stdin)
+    info = src.info
+    dst_w, dst_h = prof.scale or (info.width, info.height)
+    from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
+
+    sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
+    enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
+                       qscale=prof.qscale, sar=sar, max_batch=BATCH)
+    prog = Progress(stderr, info.fps, prof.qscale)
+    prog.duration(src.duration)
+    mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)
+
+    # two page-locked batches: the reader fills one while the GPU encodes the other
+    fb = enc.frame_bytes
+    bufs = [PinnedBuffer(BATCH * fb) for _ in range(2)]
+    free: "queue.Queue[int]" = queue.Queue()
+    full: "queue.Queue" = queue.Queue()
+    for i in range(2):
+        free.put(i)
+
+    def reader():
+        try:
+            while True:
+                i = free.get()
+                if i < 0:
+                    return
+                n = src.read_into(bufs[i].array, BATCH)
+                full.put((i, n))
+                if n < BATCH:
+                    full.put(None)
+                    return
+        except BaseException as e:   # surfaced by the main loop
+            full.put(e)
+
+    th = threading.Thread(target=reader, daemon=True)
+    th.start()
+    frames = 0
+    try:
+        while True:
+            item = full.get()
+            if item is None:
+                break
+            if isinstance(item, BaseException):
+                raise item
+            i, n = item
+            if n:
+                enc.submit(bufs[i].array[: n * fb], n)
+                packets = enc.fetch()
+                free.put(i)
+                for p in packets:
+                    mkv.write_frame(p)
+                frames += n
+                prog.update(frames, sum(len(p) for p in packets))
+            else:
+                free.put(i)
+        mkv.close()
+        prog.update(frames, 0, final=True)
+    finally:
+        free.put(-1)
+        enc.close()
+        for b in bufs:
+            b.free()
+    rc = src.close()
+    if rc:
+        stderr.write(f"decoder exited with {rc}\n")
+        return 1
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="ffmpeg_distributed_amd.worker", add_help=True)
+    ap.add_argument("--device", type=int, required=True)
+    ns, rest = ap.parse_known_args(argv)
+    try:
+        return run(ns.device, rest)
+    except Exception as e:  # the dispatcher re-queues the segment on a nonzero exit
+        sys.stderr.write(f"gpu:{ns.device}: {type(e).__name__}: {e}\n")
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,76 @@
+"""The gpu:N worker end to end on the GPU: a segment in (YUV4MPEG2 or raw Matroska), a
+V_MJPEG Matroska segment out, every packet byte-identical to the CPU oracle's encode
+of the same frame (oracle/mjpeg_oracle.c restating ffmpeg's mjpeg/swscale path)."""
+import io
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from ffmpeg_distributed_amd import container, profile, worker
+from ffmpeg_distributed_amd.encoder import split_i420
+from ffmpeg_distributed_amd.testsrc import testsrc2_i420 as make_testsrc
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+ARGS = "-c:v mjpeg -q:v {q} -dct int -huffman default -bitexact".split()
+
+
+def _args(q, scale=None):
+    a = [x.format(q=q) for x in ARGS]
+    return (["-vf", f"scale={scale[0]}:{scale[1]}:flags=bicubic"] if scale else []) + a
+
+
+def _run(data, args, monkeypatch, batch=None):
+    if batch:
+        monkeypatch.setattr(worker, "BATCH", batch)
+    out, err = io.BytesIO(), io.StringIO()
+    rc = worker.run(0, args, stdin=io.BytesIO(data), stdout=out, stderr=err)
+    assert rc == 0, err.getvalue()
+    r = container.MkvReader(io.BytesIO(out.getvalue()))
+    return r, [d for _, d in r.frames(1)], err.getvalue()
+
+
+def _y4m(frames, w, h, extra=""):
+    b = io.BytesIO()
+    b.write(f"YUV4MPEG2 W{w} H{h} F25:1 Ip A1:1 C420jpeg{extra}\n".encode())
+    for f in frames:
+        b.write(b"FRAME\n" + f.tobytes())
+    return b.getvalue()
+
+
+@pytest.mark.parametrize("w,h,scale,q,n,batch", [
+    (160, 96, None, 5, 11, 4),            # batches of 4 with a ragged tail
+    (176, 100, (96, 54), 3, 6, 32),       # downscale, odd chroma height
+    (64, 48, (130, 74), 9, 5, 2),         # upscale
+])
+def test_worker_y4m_matches_oracle(w, h, scale, q, n, batch, monkeypatch):
+    frames = [make_testsrc(w, h, i) for i in range(n)]
+    r, packets, err = _run(_y4m(frames, w, h), _args(q, scale), monkeypatch, batch)
+    dw, dh = scale or (w, h)
+    info = r.info(1)
+    assert (info.width, info.height, info.codec, info.fps) == (dw, dh, "V_MJPEG", Fraction(25))
+    assert len(packets) == n
+    for i, f in enumerate(frames):
+        y, u, v = split_i420(f, w, h)
+        sar = profile.scaled_sar((1, 1), (w, h), (dw, dh))
+        ref = oracle.encode_frame(y, u, v, dw, dh, full_range=False, qscale=q, sar=sar)
+        assert packets[i] == ref, f"frame {i}"
+    assert f"frame={n:5d}" in err
+
+
+def test_worker_raw_mkv_full_range(monkeypatch):
+    w, h, n = 96, 64, 7
+    frames = [make_testsrc(w, h, 3 + i) for i in range(n)]
+    buf = io.BytesIO()
+    wr = container.MkvWriter(buf, w, h, Fraction(30000, 1001), codec="V_UNCOMPRESSED",
+                             colour_space=b"I420", colour_range=2)
+    for f in frames:
+        wr.write_frame(f.tobytes())
+    wr.close()
+    r, packets, _ = _run(buf.getvalue(), _args(4), monkeypatch, 3)
+    assert r.info(1).fps == Fraction(30000, 1001)
+    for i, f in enumerate(frames):
+        y, u, v = split_i420(f, w, h)
+        assert packets[i] == oracle.encode_frame(y, u, v, full_range=True, qscale=4, sar=(1, 1))

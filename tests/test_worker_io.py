@@ -1,0 +1,224 @@
+"""Host side of the gpu:N worker: remote_args profile parsing, the native Matroska /
+YUV4MPEG2 segment I/O, the decoder-child replay and the passthrough to real ffmpeg.
+No GPU (the encode itself is covered by test_gpu_worker.py)."""
+import io
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import textwrap
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from ffmpeg_distributed_amd import container, profile, worker
+from ffmpeg_distributed_amd.testsrc import testsrc2_i420 as make_testsrc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+NORTH_STAR = "-vf scale=1920:1080:flags=bicubic -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact"
+
+
+# ------------------------------------------------------------------ profile
+def test_profile_north_star():
+    p = profile.parse(NORTH_STAR)
+    assert p.scale == (1920, 1080) and p.qscale == 5 and p.sws_flags == ("bicubic",)
+    p = profile.parse("-c:v mjpeg -q:v 2 -dct int -huffman default -flags +bitexact -an")
+    assert p.scale is None and p.qscale == 2
+
+
+@pytest.mark.parametrize("q,expect", [(1, 2), (2, 2), (3, 3), (5, 5), (31, 31), (40, 31), (4.5, 5), (4.4, 4), (7.9, 8)])
+def test_profile_qscale_mapping(q, expect):
+    # update_qscale: lambda = q*118 (truncated), qscale = (lambda*139 + 8192) >> 14
+    assert profile.effective_qscale(q) == expect
+
+
+@pytest.mark.parametrize("args", [
+    "-c:v libx264 -crf 18",
+    "-c:v mjpeg -q:v 5 -dct int -huffman optimal -bitexact",
+    "-c:v mjpeg -q:v 5 -huffman default -bitexact",                  # default dct is not int
+    "-c:v mjpeg -q:v 5 -dct int -huffman default",                   # no -bitexact
+    "-c:v mjpeg -b:v 10M -dct int -huffman default -bitexact",       # rate control
+    "-vf scale=1920:-2 -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
+    "-vf scale=1280:720:flags=lanczos -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
+    "-vf scale=1280:720,hflip -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -pix_fmt yuvj422p",
+])
+def test_profile_rejects_outside_gpu_path(args):
+    prof, why = profile.try_parse(args)
+    assert prof is None and why
+
+
+# ------------------------------------------------------------------ matroska
+def _mjpeg_like(i):
+    return bytes([0xFF, 0xD8]) + bytes([i & 0xFF]) * (100 + 37 * i) + bytes([0xFF, 0xD9])
+
+
+@pytest.mark.parametrize("fps", [Fraction(25), Fraction(30000, 1001), Fraction(60)])
+def test_mkv_roundtrip(fps):
+    buf = io.BytesIO()
+    w = container.MkvWriter(buf, 1920, 1080, fps, sar=(4, 3))
+    frames = [_mjpeg_like(i) for i in range(150)]      # > 1 s: several clusters
+    for f in frames:
+        w.write_frame(f)
+    w.close()
+    raw = buf.getvalue()
+    assert raw[:4] == b"\x1a\x45\xdf\xa3" and raw.count(b"\x1f\x43\xb6\x75") >= 2
+    r = container.MkvReader(io.BytesIO(raw))
+    got = list(r.frames(1))
+    assert [d for _, d in got] == frames
+    assert [t for t, _ in got] == [round(Fraction(1000 * i) / fps) for i in range(150)]
+    info = r.info(1)
+    assert (info.width, info.height, info.codec) == (1920, 1080, "V_MJPEG")
+    assert info.fps == fps
+    assert info.sar == (4, 3)
+
+
+def test_ebml_sizes():
+    assert container._size_bytes(0) == b"\x80"
+    assert container._size_bytes(126) == b"\xfe"
+    assert container._size_bytes(127) == b"\x40\x7f"        # 0x7f alone would mean "unknown"
+    assert container._size_bytes(16382) == b"\x7f\xfe"
+    assert container._size_bytes(16383) == b"\x20\x3f\xff"
+    for n in (0, 1, 126, 127, 300, 1 << 20, (1 << 28) + 5):
+        v, ln = container._read_vint(io.BytesIO(container._size_bytes(n)), False)
+        assert v == n and ln == len(container._size_bytes(n))
+
+
+def _i420(w, h, n, seed=0):
+    return np.stack([make_testsrc(w, h, seed + i) for i in range(n)])
+
+
+def _y4m(frames, w, h, fps="25:1", extra=" Ip A1:1 C420jpeg XYSCSS=420JPEG"):
+    out = io.BytesIO()
+    out.write(f"YUV4MPEG2 W{w} H{h} F{fps}{extra}\n".encode())
+    for f in frames:
+        out.write(b"FRAME\n")
+        out.write(f.tobytes())
+    return out.getvalue()
+
+
+def test_y4m_reader():
+    w, h = 70, 38                                       # odd chroma: cw = 35, ch = 19
+    fr = _i420(w, h, 5)
+    data = _y4m(fr, w, h, "30000:1001", " Ip A16:15 C420mpeg2 XCOLORRANGE=FULL")
+    rd = container.Y4MReader(io.BytesIO(data))
+    assert (rd.info.width, rd.info.height, rd.info.fps, rd.info.sar, rd.info.full_range) == \
+        (w, h, Fraction(30000, 1001), (16, 15), True)
+    buf = np.zeros((8, fr.shape[1]), np.uint8)
+    assert rd.read_into(buf, 3) == 3 and rd.read_into(buf[3:], 5) == 2
+    np.testing.assert_array_equal(buf[:5], fr)
+
+
+def test_y4m_rejects_non_420():
+    with pytest.raises(ValueError):
+        container.Y4MReader(io.BytesIO(b"YUV4MPEG2 W16 H16 F25:1 C444\n"))
+
+
+def _mkv_raw(frames, w, h, codec="V_UNCOMPRESSED", colour=b"I420", rng=1):
+    buf = io.BytesIO()
+    wr = container.MkvWriter(buf, w, h, Fraction(25), codec=codec, colour_space=colour, colour_range=rng)
+    for f in frames:
+        wr.write_frame(f.tobytes())
+    wr.close()
+    return buf.getvalue()
+
+
+def test_source_reads_uncompressed_mkv():
+    w, h = 48, 32
+    fr = _i420(w, h, 7)
+    src = worker.Source(io.BytesIO(_mkv_raw(fr, w, h, rng=2)))
+    assert src.child is None and src.info.full_range and (src.info.width, src.info.height) == (w, h)
+    buf = np.zeros((4, fr.shape[1]), np.uint8)
+    out = []
+    while True:
+        n = src.read_into(buf, 4)
+        out.extend(buf[:n].copy())
+        if n < 4:
+            break
+    np.testing.assert_array_equal(np.stack(out), fr)
+
+
+FAKE_DECODER = textwrap.dedent("""
+    import sys
+    sys.path.insert(0, {root!r})
+    from ffmpeg_distributed_amd import container
+    r = container.MkvReader(sys.stdin.buffer)
+    i = r.info(1)
+    o = sys.stdout.buffer
+    o.write(b"YUV4MPEG2 W%d H%d F25:1 Ip A1:1 C420jpeg XCOLORRANGE=LIMITED\\n" % (i.width, i.height))
+    for _, d in r.frames(1):
+        o.write(b"FRAME\\n" + d[::-1][::-1])
+""")
+
+
+def test_source_decoder_child_gets_every_byte(monkeypatch, tmp_path):
+    """Non-raw codecs go through a decoder child; the bytes the Matroska probe already
+    consumed must be replayed to it (here the 'codec' is raw I420 under another name)."""
+    w, h = 64, 48
+    fr = _i420(w, h, 40)
+    script = tmp_path / "fake_decoder.py"
+    script.write_text(FAKE_DECODER.format(root=ROOT))
+    monkeypatch.setattr(worker, "DECODE_ARGV", [sys.executable, str(script)])
+    src = worker.Source(io.BytesIO(_mkv_raw(fr, w, h, codec="V_MPEG4/ISO/AVC", colour=b"")))
+    assert src.child is not None and not src.info.full_range
+    buf = np.zeros((64, fr.shape[1]), np.uint8)
+    n = src.read_into(buf, 64)
+    assert n == 40
+    np.testing.assert_array_equal(buf[:40], fr)
+    assert src.close() == 0
+
+
+def test_worker_passthrough_runs_reference_command(tmp_path):
+    """remote_args outside the GPU profile: exactly the reference's worker ffmpeg runs."""
+    log = tmp_path / "shim.log"
+    env = dict(os.environ, PATH=os.path.join(HERE, "shims") + os.pathsep + os.environ["PATH"],
+               SHIM_LOG=str(log), PYTHONPATH=ROOT)
+    args = ["-c:v", "libx264", "-crf", "18"]
+    p = subprocess.run([sys.executable, "-m", "ffmpeg_distributed_amd.worker", "--device", "0", *args],
+                       input=b"SEGMENT", capture_output=True, env=env, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout == b"ENC[SEGMENT]"
+    calls = [json.loads(l) for l in open(log)]
+    assert calls == [{"prog": "ffmpeg", "argv": worker.reference_argv(args)[1:], "host": "localhost"}]
+    assert b"running ffmpeg on the CPU" in p.stderr
+
+
+def test_progress_lines_parse_with_dispatcher_regex():
+    from ffmpeg_distributed_amd import dispatcher as D
+    err = io.StringIO()
+    pr = worker.Progress(err, Fraction(25), 5)
+    pr.duration(12.5)
+    pr.update(250, 123456, final=True)
+    lines = err.getvalue().splitlines()
+    assert D.parse_duration(lines[0]) == pytest.approx(12.5)
+    f, fps, t, speed = D.parse_progress(lines[1])
+    assert f == 250 and t == pytest.approx(10.0) and speed > 0
+
+
+def test_scaled_sar_follows_vf_scale():
+    assert profile.scaled_sar((1, 1), (3840, 2160), (1920, 1080)) == (1, 1)
+    assert profile.scaled_sar((1, 1), (176, 100), (96, 54)) == (99, 100)
+    assert profile.scaled_sar((0, 0), (176, 100), (96, 54)) == (0, 0)
+    assert profile.scaled_sar((4, 3), (720, 576), (1280, 720)) == (15, 16)
+
+
+@pytest.mark.parametrize("num,den,mx", [(1, 1, 65535), (100000, 70001, 65535), (355, 113, 100),
+                                        (2**40 + 1, 2**39, 65535), (-6, 4, 10), (65536, 65535, 65535)])
+def test_av_reduce_bounds_and_accuracy(num, den, mx):
+    n, d = profile.av_reduce(num, den, mx)
+    assert abs(n) <= mx and 0 < d <= mx
+    x = Fraction(num, den)
+    if abs(x.numerator) <= mx and x.denominator <= mx:
+        assert Fraction(n, d) == x                       # exact when it fits
+    assert abs(Fraction(n, d) - x) <= abs(x) / mx
+
+
+def test_mkv_without_display_size_means_square_pixels():
+    buf = io.BytesIO()
+    w = container.MkvWriter(buf, 320, 240, Fraction(25))
+    w.write_frame(b"x")
+    w.close()
+    assert container.MkvReader(io.BytesIO(buf.getvalue())).info(1).sar == (1, 1)
