@@ -95,6 +95,7 @@ def main():
     from ffmpeg_distributed_amd import build as B
     B.build()
     from ffmpeg_distributed_amd.encoder import MjpegEncoder
+    from ffmpeg_distributed_amd.shard import max_over_ranks, segments_for_rank, timed_region
     from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
 
     torch.cuda.set_device(local)
@@ -107,19 +108,23 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # resident input pool: distinct frames, different per rank (rank's own segments)
+    # The job is (warmup + steps) x world segments of `seg` frames, split round-robin over
+    # ranks (shard.segments_for_rank).  Each rank keeps a resident pool of its first
+    # segments' frames (testsrc2-like, time index = global frame number) and cycles it.
     seg = a.seg
-    pool_n = max(seg, (a.pool // seg) * seg)
+    my_segs = segments_for_rank((a.warmup + a.steps) * world, rank, world)
+    nseg_pool = max(1, min(len(my_segs), a.pool // seg))
+    pool_n = nseg_pool * seg
     fb = W * H * 3 // 2
     pool = torch.empty((pool_n, fb), dtype=torch.uint8, device=dev)
     gen = 20
-    for i in range(0, pool_n, gen):
-        k = min(gen, pool_n - i)
-        pool[i:i + k] = testsrc2_i420_torch(W, H, rank * 100000 + i, k, dev)
+    for j in range(nseg_pool):
+        for i in range(0, seg, gen):
+            k = min(gen, seg - i)
+            pool[j * seg + i: j * seg + i + k] = testsrc2_i420_torch(W, H, my_segs[j] * seg + i, k, dev)
     torch.cuda.synchronize()
 
     enc = MjpegEncoder(local, W, H, qscale=Q, max_batch=seg, timing=True)
-    nseg_pool = pool_n // seg
     bytes_out = []
 
     def step(s):
@@ -128,24 +133,13 @@ def main():
         sizes = enc.sync()
         bytes_out.append(int(sizes.sum()))
 
-    for s in range(a.warmup):
-        step(s)
-    enc.kernel_times(reset=True)
-    bytes_out.clear()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(a.steps):
-        step(a.warmup + s)
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    kt, nl = enc.kernel_times()
+    def reset():
+        enc.kernel_times(reset=True)
+        bytes_out.clear()
 
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = timed_region(step, a.warmup, a.steps, barrier, torch.cuda.synchronize, reset)
+    kt, nl = enc.kernel_times()
+    dt = max_over_ranks(dt, dist if world > 1 else None, dev)
 
     frames_total = a.steps * seg * world
     value = frames_total / dt

@@ -23,6 +23,7 @@ MJG_E_STATE = -5
 MJG_F_TIMING = 1
 MJG_F_DEBUG_COEFS = 2
 MJG_F_SWS_NO_BITEXACT = 4
+MJG_F_COM_ITU601 = 8
 
 KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write")
 MJG_NUM_KERNELS = len(KERNEL_NAMES)
@@ -109,10 +110,11 @@ def device_count() -> int:
     return check(load().mjg_device_count())
 
 
-def build_header(dst_w: int, dst_h: int, qscale: int, sar=(1, 1)) -> bytes:
+def build_header(dst_w: int, dst_h: int, qscale: int, sar=(1, 1), com_itu601: bool = False) -> bytes:
     """The per-config JPEG header, computed on the host (no GPU needed)."""
     L = load()
-    cfg = MjgConfig(dst_w, dst_h, dst_w, dst_h, 1, qscale, sar[0], sar[1], 1, 0)
+    cfg = MjgConfig(dst_w, dst_h, dst_w, dst_h, 1, qscale, sar[0], sar[1], 1,
+                    MJG_F_COM_ITU601 if com_itu601 else 0)
     n = C.c_size_t()
     check(L.mjg_build_header(C.byref(cfg), None, 0, C.byref(n)))
     buf = (C.c_uint8 * n.value)()

@@ -45,7 +45,8 @@ struct ByteWriter {
   void u16(int v) { u8(v >> 8); u8(v); }
 };
 
-std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sar_num, int sar_den) {
+std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sar_num, int sar_den,
+                                  bool com_itu601) {
   ByteWriter o;
   o.u16(0xFFD8);
   if (sar_num > 0 && sar_den > 0) {
@@ -58,6 +59,11 @@ std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sa
     o.u16(sar_den);
     o.u8(0);
     o.u8(0);
+  }
+  if (com_itu601) {  // jpeg_put_comments: COM "CS=ITU601" when the encoder pix_fmt is yuv420p
+    o.u16(0xFFFE);
+    o.u16(12);
+    for (char ch : {'C', 'S', '=', 'I', 'T', 'U', '6', '0', '1', '\0'}) o.u8(ch);
   }
   o.u16(0xFFDB);
   o.u16(2 + 65);
@@ -274,7 +280,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     c->mprime[i] = (uint8_t)v;
     c->qmat[i] = (int32_t)((2ull << 21) / (uint64_t)(16 * v));
   }
-  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den);
+  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0);
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row])
@@ -562,12 +568,15 @@ int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *le
   if (cfg->dst_w < 1 || cfg->dst_h < 1 || cfg->dst_w > 65535 || cfg->dst_h > 65535 ||
       cfg->qscale < 1 || cfg->qscale > 31)
     return set_err(MJG_E_INVALID, "bad size / qscale");
+  if (cfg->sar_num < 0 || cfg->sar_den < 0 || cfg->sar_num > 65535 || cfg->sar_den > 65535)
+    return set_err(MJG_E_INVALID, "bad SAR %d:%d", cfg->sar_num, cfg->sar_den);
   uint8_t mp[64];
   for (int i = 0; i < 64; i++) {
     const int v = i == 0 ? 8 : ((kMpeg1Intra[i] * cfg->qscale) >> 3);
     mp[i] = (uint8_t)(v > 255 ? 255 : v);
   }
-  const std::vector<uint8_t> h = build_header(cfg->dst_w, cfg->dst_h, mp, cfg->sar_num, cfg->sar_den);
+  const std::vector<uint8_t> h = build_header(cfg->dst_w, cfg->dst_h, mp, cfg->sar_num, cfg->sar_den,
+                                             (cfg->flags & MJG_F_COM_ITU601) != 0);
   if (len) *len = h.size();
   if (!out) return MJG_OK;
   if (cap < h.size()) return set_err(MJG_E_CAPACITY, "header needs %zu bytes", h.size());

@@ -41,7 +41,7 @@ class MjpegEncoder:
     def __init__(self, device: int, src_w: int, src_h: int, dst_w: Optional[int] = None,
                  dst_h: Optional[int] = None, full_range: bool = False, qscale: int = 5,
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
-                 debug_coefs: bool = False, sws_bitexact: bool = True):
+                 debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -55,6 +55,8 @@ class MjpegEncoder:
             flags |= _lib.MJG_F_DEBUG_COEFS
         if not sws_bitexact:
             flags |= _lib.MJG_F_SWS_NO_BITEXACT
+        if com_itu601:
+            flags |= _lib.MJG_F_COM_ITU601
         sar = sar or (0, 0)
         cfg = MjgConfig(self.src_w, self.src_h, self.dst_w, self.dst_h, int(bool(full_range)),
                         int(qscale), int(sar[0]), int(sar[1]), self.max_batch, flags)

@@ -30,6 +30,9 @@ from . import container, profile
 DECODE_ARGV = ["ffmpeg", "-v", "error", "-f", "matroska", "-i", "pipe:", "-map", "0:v:0",
                "-f", "yuv4mpegpipe", "-strict", "-1", "pipe:"]
 BATCH = int(os.environ.get("MJG_WORKER_BATCH", "32"))
+# FFmpeg builds differ in the pix_fmt their CLI hands the mjpeg encoder for yuv420p input
+# (yuvj420p: no COM; yuv420p + full range: COM "CS=ITU601"); default = yuvj420p.
+COM_ITU601 = os.environ.get("MJG_COM_ITU601", "0") == "1"
 
 
 def reference_argv(args: List[str]) -> List[str]:
@@ -170,7 +173,8 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
-                       qscale=prof.qscale, sar=sar, max_batch=BATCH)
+                       qscale=prof.qscale, sar=sar, max_batch=BATCH,
+                       com_itu601=COM_ITU601 and not info.full_range)
     prog = Progress(stderr, info.fps, prof.qscale)
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)

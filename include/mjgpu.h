@@ -40,6 +40,9 @@ extern "C" {
 #define MJG_F_TIMING 1u        /* record HIP events around every kernel launch */
 #define MJG_F_DEBUG_COEFS 2u   /* keep quantized coefficients of every block (tests) */
 #define MJG_F_SWS_NO_BITEXACT 4u /* swscale filter tables without SWS_BITEXACT */
+#define MJG_F_COM_ITU601 8u    /* add COM "CS=ITU601" (FFmpeg builds whose CLI hands the encoder
+                                  yuv420p+full-range instead of yuvj420p; mjpegenc_common.c
+                                  jpeg_put_comments) */
 
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane)        */

@@ -1,0 +1,107 @@
+"""The N>1 path on the CPU: two gloo ranks run the same sharding / timed-region / max
+reduction code bench.py runs over RCCL, and the dispatcher drives two `gpu:N` hosts
+(worker stubbed) so segments are split across devices with no collective."""
+import os
+import socket
+import time
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ffmpeg_distributed_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    done = []
+    segs = shard.segments_for_rank(12, rank, world)
+    # rank 1 is slower: the job time must be its time, seen identically by both ranks
+    dt = shard.timed_region(lambda s: (done.append(segs[s]), time.sleep(0.01 * (1 + rank))),
+                            1, len(segs) - 1, dist.barrier, lambda: None)
+    mx = shard.max_over_ranks(dt, dist)
+    q.put((rank, segs, done, dt, mx))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_gloo_ranks_shard_and_reduce():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    all_segs = sorted(s for _, segs, _, _, _ in res for s in segs)
+    assert all_segs == list(range(12))                     # every segment exactly once
+    assert all(done == segs for _, segs, done, _, _ in res)
+    mx = {r[4] for r in res}
+    assert len(mx) == 1 and mx.pop() == pytest.approx(max(r[3] for r in res))
+    # the closing barrier makes the fast rank wait: both see at least the slow rank's work
+    slow_work = (len(res[1][1]) - 1) * 0.02
+    assert min(r[3] for r in res) >= slow_work * 0.95
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (1, 8), (300, 8), (7, 3)])
+def test_round_robin_partition(n, world):
+    parts = [shard.segments_for_rank(n, r, world) for r in range(world)]
+    assert sorted(s for p in parts for s in p) == list(range(n))
+    assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def test_single_rank_max_is_identity():
+    assert shard.max_over_ranks(1.25) == 1.25
+
+
+STUB_WORKER = r"""
+import sys, time
+dev = sys.argv[sys.argv.index("--device") + 1]
+data = sys.stdin.read()
+time.sleep(0.2)
+sys.stderr.write("  Duration: 00:00:02.00, start: 0.000000, bitrate: N/A\n")
+sys.stderr.write("frame=   50 fps= 25 q=5.0 size=N/A time=00:00:02.00 bitrate=N/A speed=1.00x\n")
+sys.stdout.write("GPU" + dev + "[" + data + "]")
+"""
+
+
+def test_dispatcher_spreads_segments_over_gpu_hosts(tmp_path, monkeypatch):
+    """-H gpu:0 -H gpu:1: every segment is encoded exactly once, by one of the two
+    device workers, pulled dynamically from the shared queue; no collective involved."""
+    import sys
+    from ffmpeg_distributed_amd import dispatcher as D
+    here = os.path.dirname(os.path.abspath(__file__))
+    monkeypatch.setenv("PATH", os.path.join(here, "shims") + os.pathsep + os.environ["PATH"])
+    monkeypatch.setenv("SHIM_SEGMENTS", "6")
+    monkeypatch.chdir(tmp_path)
+    stub = tmp_path / "stub_worker.py"
+    stub.write_text(STUB_WORKER)
+    real = D.worker_argv
+
+    def argv(host, args):
+        a = real(host, args)
+        assert a[:3] == [sys.executable, "-m", "ffmpeg_distributed_amd.worker"]
+        return [sys.executable, str(stub)] + a[3:]
+
+    monkeypatch.setattr(D, "worker_argv", argv)
+    (tmp_path / "input.mp4").write_text("RAW")
+    D.encode(["gpu:0", "gpu:1"], "input.mp4", "out.mkv", 2, "-c:v mjpeg -q:v 5", "-an",
+             tmp_dir="segs", keep_tmp=True)
+    outs = sorted(os.listdir(tmp_path / "segs" / "out"))
+    assert outs == [f"{i:08d}.mkv" for i in range(6)]
+    bodies = [(tmp_path / "segs" / "out" / o).read_text() for o in outs]
+    assert all(b.startswith(("GPU0[SEG", "GPU1[SEG")) for b in bodies)
+    assert {b[:4] for b in bodies} == {"GPU0", "GPU1"}
+    assert (tmp_path / "out.mkv").read_text() == "|".join(bodies)

@@ -191,6 +191,8 @@ def test_header_layout(q, sar):
 def test_library_header_equals_oracle():
     for (w, h, q, sar) in [(1920, 1080, 5, (1, 1)), (72, 40, 2, (0, 0)), (3840, 2160, 31, (4, 3))]:
         assert _lib.build_header(w, h, q, sar) == oracle.header(w, h, q, sar=sar)
+        assert _lib.build_header(w, h, q, sar, com_itu601=True) == \
+            oracle.header(w, h, q, sar=sar, com_itu601=True)
 
 
 # -------------------------------------------------------------------- full frames
