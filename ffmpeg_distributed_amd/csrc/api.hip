@@ -147,7 +147,7 @@ struct mjg_ctx {
   uint8_t *d_stage = nullptr, *d_scaled = nullptr;
   uint32_t *d_scratch = nullptr;
   uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_chunk_ff = nullptr, *d_ff_off = nullptr;
-  uint32_t *d_frame_bits = nullptr, *d_status = nullptr;
+  uint32_t *d_frame_bits = nullptr, *d_status = nullptr, *d_work = nullptr;
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
@@ -173,7 +173,7 @@ void free_ctx(mjg_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
-                  c->d_chunk_off, c->d_chunk_ff, c->d_ff_off, c->d_frame_bits, c->d_status,
+                  c->d_chunk_off, c->d_chunk_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
                   c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->ps[0].hc,
                   c->ps[0].vc, c->ps[0].hp, c->ps[0].vp, c->ps[1].hc, c->ps[1].vc, c->ps[1].hp,
                   c->ps[1].vp};
@@ -301,13 +301,18 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
       (rc = dmalloc(&c->d_chunk_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
       (rc = dmalloc(&c->d_frame_bits, B)) || (rc = dmalloc(&c->d_status, 4)) ||
+      (rc = dmalloc(&c->d_work, 1)) ||
       (rc = dmalloc(&c->d_frame_size, B)) || (rc = dmalloc(&c->d_frame_offsets, B + 1)))
     return rc;
   c->out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096);
   if ((rc = dmalloc(&c->d_out, c->out_cap))) return rc;
   if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
   if (g.debug_coefs && (rc = dmalloc(&c->d_dbg, B * (size_t)g.nmcu * 6 * 64))) return rc;
+#ifdef MJG_STAMPS
+  if (!c->d_dbg && (rc = dmalloc(&c->d_dbg, (size_t)1 << 22))) return rc;  // 512K stamps
+#endif
   HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(c->d_work, 0, sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipHostMalloc((void **)&c->h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void **)&c->h_status, 16, hipHostMallocDefault));
@@ -334,7 +339,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // persistent k_encode grid: every CU filled with as many workgroups as fit
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode, 64 * kWavesPerWg, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true>, 64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
 
   c->timing = (k.flags & MJG_F_TIMING) != 0;
@@ -452,12 +457,17 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_ENCODE, 0);
   const int ntasks = g.nchunks * n;
   const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
-  k_encode<<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
-                                                    c->d_chunk_bits, c->d_dbg, ntasks);
+  if (g.range_convert)
+    k_encode<true><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
+                                                      c->d_chunk_bits, c->d_dbg, c->d_work, ntasks);
+  else
+    k_encode<false><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
+                                                      c->d_chunk_bits, c->d_dbg, c->d_work, ntasks);
   tmark(c, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_BITS, 0);
-  k_scan_bits<<<n, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, g.nchunks);
+  k_scan_bits<<<n, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, g.nchunks,
+                                         c->d_work);
   tmark(c, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_COUNT_FF, 0);
@@ -605,11 +615,9 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   const size_t nb = (size_t)c->geom.nmcu * 6;  // dbg buffer: frame-major, block order
   if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
-  std::vector<int16_t> zz(nb * 64);  // kernel stores zigzag order
-  HIP_TRY(hipMemcpy(zz.data(), c->d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
+  // the kernel stores each quantised block in natural (raster) order
+  HIP_TRY(hipMemcpy(out, c->d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
                     hipMemcpyDeviceToHost));
-  for (size_t b = 0; b < nb; b++)
-    for (int k = 0; k < 64; k++) out[b * 64 + kZigzag[k]] = zz[b * 64 + k];
   return MJG_OK;
 }
 
@@ -639,3 +647,11 @@ int mjg_debug_filter(mjg_ctx *c, int plane, int dir, int16_t *coeff, int32_t *po
 }
 
 }  // extern "C"
+
+#ifdef MJG_STAMPS
+extern "C" int mjg_debug_stamps(mjg_ctx *c, uint64_t *out, size_t n) {
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, c->d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return MJG_OK;
+}
+#endif

@@ -22,7 +22,7 @@
 #include "jpeg_tables.h"
 
 #ifndef MJG_ENC_WAVES_PER_EU
-#define MJG_ENC_WAVES_PER_EU 4  // k_encode occupancy target (waves per SIMD); measured best
+#define MJG_ENC_WAVES_PER_EU 3  // k_encode occupancy target (waves per SIMD); measured best (v8)
 #endif
 #ifndef MJG_ABLATE
 #define MJG_ABLATE 0  // perf experiments only: 1 = no bit-pack
@@ -192,7 +192,8 @@ struct RegSink {
 // (Mean nonzero AC per block is ~1.2 on testsrc2 4K q5, so the loop is short.)
 template <int STRIDE, class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask, int diff,
-                                           const uint32_t *ac, const uint32_t *dc, Sink &sink) {
+                                           const uint32_t *ac, const uint32_t *dc,
+                                           const uint8_t *zz, Sink &sink) {
   {
     const int cat = dc_cat(diff);
     const uint32_t e = dc[cat];
@@ -203,7 +204,8 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask,
   while (mask) {
     const int k = (int)__builtin_ctzll(mask);
     mask &= mask - 1;
-    const int v = (int)(int16_t)(pkcol[(k >> 1) * STRIDE] >> (16 * (k & 1)));
+    const int n = zz[k];  // natural index of zigzag position k
+    const int v = (int)(int16_t)(pkcol[(n >> 1) * STRIDE] >> (16 * (n & 1)));
     int run = k - prev - 1;
     prev = k;
     while (run >= 16) {
@@ -293,20 +295,64 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
   return s;
 }
 
+#ifndef MJG_ENC_BATCH
+#define MJG_ENC_BATCH 16
+#endif
+constexpr int kBatch = MJG_ENC_BATCH;  // chunks per work unit pulled from the counter
+
+// DC predictor carried into a chunk that does not follow this wave's previous chunk: the
+// quantised DCs of the 6 blocks before it (the only possible predecessors), lane 58+i
+// holding block chunk*64-6+i.  Quantised DC = (pixel sum + 32) >> 6 exactly.
+// carry_row: lanes 0..47 load row (lane & 7) of block (lane >> 3) of those 6 blocks
+// (issued early so the load overlaps a chunk's work); carry_finish reduces them.
+__device__ __forceinline__ uint64_t carry_row(const uint8_t *frames, const EncGeom &g, int frame,
+                                              int chunk, int lane) {
+  if (chunk == 0 || lane >= 48) return 0;
+  const Src s = block_src(frames, g, frame, chunk * 64 - 6 + (lane >> 3));
+  const uint8_t *row = s.plane + (size_t)min(s.y0 + (lane & 7), s.ph - 1) * s.stride;
+  if (s.x0 + 8 <= s.pw && (((uintptr_t)(row + s.x0)) & 7) == 0)
+    return *(const uint64_t *)(row + s.x0);
+  uint64_t w = 0;
+  for (int x = 0; x < 8; x++) w |= (uint64_t)row[min(s.x0 + x, s.pw - 1)] << (8 * x);
+  return w;
+}
+
+__device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, bool rc) {
+  if (chunk == 0) return 128;
+  const int pb = chunk * 64 - 6 + (lane >> 3);
+  const bool chroma = (pb - 6 * (pb / 6)) >= 4;
+  int sum = 0;
+#pragma unroll
+  for (int x = 0; x < 8; x++) {
+    const int p = (int)((w >> (8 * x)) & 255u);
+    sum += !rc ? p : (chroma ? range_chroma(p) : range_luma(p));
+  }
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
+  sum += __shfl_xor(sum, 4, 64);
+  const int d = __shfl((sum + 32) >> 6, max(lane - 58, 0) * 8, 64);
+  return lane >= 58 ? d : 128;
+}
+
+template <bool RC>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
-    int16_t *__restrict__ dbg_coefs, int ntasks) {
+    int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
+  __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ uint32_t s_win_all[kWavesPerWg][kWaveWinWords];
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
   if (tid < 32) s_dc[tid] = tabs[512 + tid];
-  if (tid < 64) s_qc[tid] = (int32_t)tabs[544 + tid];
+  if (tid < 64) {
+    s_qc[tid] = (int32_t)tabs[544 + tid];
+    s_zz[tid] = kZigzag[tid];
+  }
   uint32_t *s_win = s_win_all[wave];
   uint32_t *s_pk = s_pk_all[wave];
   for (int i = lane; i < kWaveWinWords; i += 64) s_win[i] = 0;
@@ -314,67 +360,44 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
 
   const int nwaves = gridDim.x * kWavesPerWg;
   const int gw = blockIdx.x * kWavesPerWg + wave;
-  const int per = (ntasks + nwaves - 1) / nwaves;
-  const int t0 = gw * per, t1 = min(ntasks, t0 + per);
-  if (t0 >= t1) return;
+  const int nbatch = (ntasks + kBatch - 1) / kBatch;
+#ifdef MJG_STAMPS  // diagnostic build: per-wave start/end shader clock into dbg_coefs
+  const uint64_t stamp0 = __builtin_amdgcn_s_memtime();
+  struct StampOnExit {
+    uint64_t t0;
+    uint64_t *dst;
+    int lane;
+    __device__ ~StampOnExit() {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      if (lane == 0) {
+        dst[0] = t0;
+        dst[1] = t1;
+      }
+    }
+  } stamp_guard{stamp0, (uint64_t *)dbg_coefs + 2 * gw, lane};
+#endif
+  if (gw >= nbatch) return;
   const int nblk = g.nmcu * 6;
   const int nck = (nblk + 63) >> 6;
-  const bool rc = g.range_convert != 0;
+  constexpr bool rc = RC;
 
-  // first chunk of this wave's range
-  int frame = t0 / nck, chunk = t0 - frame * nck;
+  // Batches of kBatch consecutive chunks: the first one static (batch gw), the rest
+  // pulled from work_ctr (zeroed by k_scan_bits after every launch), so waves whose
+  // picture content is cheap take more batches and all waves finish together.
+  int t = gw * kBatch, tend = min(t + kBatch, ntasks);
+  uint32_t nb = 0;  // lane 0: the batch after this one
+  if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
+  int frame = t / nck, chunk = t - frame * nck;
   int b = chunk * 64 + lane;
   bool active = b < nblk;
   uint64_t raw[8];
   bool fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
+  int carry = carry_finish(carry_row(frames, g, frame, chunk, lane), chunk, lane, rc);
 
-  // DC carry: quantised DCs of the 64 blocks before this chunk (lane i = block chunk*64-64+i)
-  int carry = 128;
-  if (chunk > 0) {
-    for (int i = 0; i < 6; i++) {  // only blocks chunk*64-6 .. -1 can be predecessors
-      const int pb = chunk * 64 - 6 + i;
-      const Src s = block_src(frames, g, frame, pb);
-      const int px = lane & 7, py = lane >> 3;
-      int v = s.plane[(size_t)min(s.y0 + py, s.ph - 1) * s.stride + min(s.x0 + px, s.pw - 1)];
-      const int chroma = (pb - 6 * (pb / 6)) >= 4;
-      if (rc) v = chroma ? range_chroma(v) : range_luma(v);
-      const int d = (wave_sum(v) + 32) >> 6;
-      if (lane == 58 + i) carry = d;
-    }
-  }
-
-  for (int t = t0; t < t1; t++) {
+  while (true) {
     const int blk = b - 6 * (b / 6);
     const int tab = blk < 4 ? 0 : 1;
     if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, b));
-#if MJG_ABLATE >= 8  // perf experiment: 9 = pixel loads only, 8 = loads + row pass
-    {
-      uint32_t acc = 0;
-#if MJG_ABLATE == 8
-      for (int r = 0; r < 8; r++) {
-        int cr[8];
-        for (int x = 0; x < 8; x++) cr[x] = (int)((raw[r] >> (8 * x)) & 255u);
-        fdct8<1, true>(cr);
-        for (int x = 0; x < 8; x++) acc += cr[x];
-      }
-#else
-      for (int r = 0; r < 8; r++) acc += (uint32_t)raw[r] ^ (uint32_t)(raw[r] >> 32);
-#endif
-      if (t + 1 < t1) {
-        if (++chunk == nck) {
-          chunk = 0;
-          frame++;
-        }
-        b = chunk * 64 + lane;
-        active = b < nblk;
-        fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
-      }
-      acc = wave_sum((int)acc);
-      // keep acc live but publish a valid (empty) chunk: later kernels index by these lengths
-      if (lane == 0) chunk_bits[t] = (acc == 0x9e3779b9u) ? 32u : 0u;
-      continue;
-    }
-#endif
     // unpack + tv->pc + FDCT row pass, one row at a time; the row outputs (int16 in
     // FFmpeg, and they fit) go to this wave's LDS block image as pairs [row*4+j][lane].
     // Luma and chroma share one range formula: chroma's (p*596864 - 9027848) >> 19 ==
@@ -397,15 +420,21 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // prefetch the next chunk while this one is encoded
     const int cur_frame = frame, cur_chunk = chunk;
     const bool cur_active = active;
-    if (t + 1 < t1) {
-      if (++chunk == nck) {
-        chunk = 0;
-        frame++;
-      }
+    int tn = t + 1;
+    const bool new_batch = tn >= tend;
+    if (new_batch) {
+      const int nbu = __builtin_amdgcn_readfirstlane(nb);
+      tn = nbu < nbatch ? nbu * kBatch : -1;
+    }
+    if (tn >= 0) {
+      frame = tn / nck;
+      chunk = tn - frame * nck;
       b = chunk * 64 + lane;
       active = b < nblk;
       fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
     }
+    // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
+    const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, chunk, lane) : 0;
 
     // Column pass two columns at a time from the LDS row image, each coefficient
     // quantised straight into a packed zigzag register image (qpk), which then replaces
@@ -416,9 +445,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     int dc = 0;
     uint32_t mlo = 0, mhi = 0;
     if (cur_active) {
-      uint32_t qpk[32];
-#pragma unroll
-      for (int i = 0; i < 32; i++) qpk[i] = 0;
 #pragma unroll
       for (int jp = 0; jp < 4; jp++) {
         __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
@@ -452,19 +478,18 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
               else
                 mhi |= nz << (k - 32);
             }
-            if (k & 1)
-              qpk[k >> 1] |= (uint32_t)v << 16;
-            else
-              qpk[k >> 1] |= (uint32_t)v & 0xffffu;
+            cc[h][r] = v;
           }
         }
-      }
+        // quantised pair (row r, columns 2jp, 2jp+1) replaces the row-pass pair it came
+        // from: the block image is now the quantised block in natural order
 #pragma unroll
-      for (int i = 0; i < 32; i++) s_pk[i * 64 + lane] = qpk[i];
-      if (g.debug_coefs) {  // packed zigzag pairs; the host reorders (mjg_debug_coefs)
-        uint32_t *o = (uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64);
-#pragma unroll
-        for (int k = 0; k < 32; k++) o[k] = qpk[k];
+        for (int r = 0; r < 8; r++) {
+          const uint32_t w = ((uint32_t)cc[0][r] & 0xffffu) | ((uint32_t)cc[1][r] << 16);
+          s_pk[(r * 4 + jp) * 64 + lane] = w;
+          if (g.debug_coefs)  // natural-order int16 pairs
+            ((uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64))[r * 4 + jp] = w;
+        }
       }
     }
     const uint64_t mask = ((uint64_t)mhi << 32) | mlo;
@@ -481,7 +506,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     RegSink q;
 #if MJG_ABLATE == 0
     if (cur_active) {
-      emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, q);
+      emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, q);
       q.finish();
     }
 #else
@@ -520,7 +545,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
           sink.wbase = wbase;
           sink.win = s_win;
           sink.cap = kWaveWinWords;
-          emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, sink);
+          emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, sink);
           sink.finish();
         }
       }
@@ -531,6 +556,13 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       }
     }
     if (lane == 0) chunk_bits[t] = total;
+    if (tn < 0) break;
+    if (new_batch) {
+      carry = carry_finish(crow, chunk, lane, rc);
+      tend = min(tn + kBatch, ntasks);
+      if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
+    }
+    t = tn;
   }
 }
 
@@ -568,8 +600,10 @@ __device__ uint32_t block_excl_scan(const uint32_t *in, uint32_t *out, int n) {
 // their slots (defence in depth; k_encode never writes more than a slot).
 __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk_bits,
                                                     uint32_t *__restrict__ chunk_off,
-                                                    uint32_t *__restrict__ frame_bits, int nchunks) {
+                                                    uint32_t *__restrict__ frame_bits, int nchunks,
+                                                    uint32_t *__restrict__ work_ctr) {
   const int f = blockIdx.x;
+  if (f == 0 && threadIdx.x == 0) *work_ctr = 0;  // k_encode's batch counter, for the next launch
   uint32_t *cb = chunk_bits + (size_t)f * nchunks;
   for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
   __syncthreads();

@@ -32,6 +32,7 @@ res = {
 res["read_over_input"] = res["read_bytes_per_launch"] / res["input_plane_bytes_per_launch"]
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                     "pmc_encode_4k_q5.json")
-with open(path, "w") as f:
-    json.dump(res, f, indent=1)
+for pth in (path, os.path.join(out, "pmc_encode_4k_q5.json")):  # gpurun_out/ travels back
+    with open(pth, "w") as f:
+        json.dump(res, f, indent=1)
 print(json.dumps(res, indent=1))

@@ -14,4 +14,4 @@ mkdir -p $OUT
 timeout -k 10 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/calib -o run --output-format csv -- $OUT/calib_bin 1565523968 > $OUT/calib.log 2>&1 || exit 1
 timeout -k 10 150 rocprofv3 --kernel-include-regex 'mjg::' --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 tools/pmc_workload.py > $OUT/fetch.log 2>&1 || exit 1
 timeout -k 10 150 rocprofv3 --kernel-include-regex 'mjg::' --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 tools/pmc_workload.py > $OUT/write.log 2>&1 || exit 1
-python3 tools/pmc_traffic.py $OUT 1565523968 && echo done
+python3 tools/pmc_traffic.py $OUT 1565523968 && rm -f $OUT/calib_bin && echo done
