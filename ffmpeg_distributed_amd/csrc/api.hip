@@ -283,8 +283,12 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0);
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
-  // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row])
-  uint32_t tabs[608] = {0};
+  // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
+  // [608,672) k_encode's screening thresholds B^2 (fp32 bits, [col][row]): a quantised AC
+  // coefficient is nonzero iff |u| >= T = ceil(5*2^18 / qmat) (dct_quantize_c intra
+  // rounding), i.e. |pass-2 sum| >= 16T - 8 (rows 0, 4: DESCALE 4, exact in fp32) or
+  // >= T*2^17 - 2^16 (other rows); the latter is widened by 2048 > the fp32 error (< 2^9).
+  uint32_t tabs[kTabWords] = {0};
   build_huffman(tabs, kBitsAcLum, kValAcLum);
   build_huffman(tabs + 256, kBitsAcChr, kValAcChr);
   uint32_t dc[256];
@@ -293,10 +297,18 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   build_huffman(dc, kBitsDcChr, kValDc);
   for (int i = 0; i < 16; i++) tabs[528 + i] = dc[i];
   for (int i = 0; i < 64; i++) tabs[544 + (i & 7) * 8 + (i >> 3)] = (uint32_t)c->qmat[i];  // [col][row]
+  for (int i = 1; i < 64; i++) {
+    const int ro = i >> 3;
+    const uint32_t qm = (uint32_t)c->qmat[i];
+    const double Ti = (double)(((5u << 18) + qm - 1) / qm);  // ceil(5*2^18 / qmat)
+    const double B = (ro == 0 || ro == 4) ? 16.0 * Ti - 8.5 : Ti * 131072.0 - 65536.0 - 2048.0;
+    const float b2 = (float)(B * B);
+    memcpy(&tabs[608 + (i & 7) * 8 + ro], &b2, 4);
+  }
 
   const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks;
   int rc;
-  if ((rc = dmalloc(&c->d_tabs, 608)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
+  if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
       (rc = dmalloc(&c->d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
       (rc = dmalloc(&c->d_chunk_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
@@ -357,14 +369,14 @@ void tmark(mjg_ctx *c, int k, int end) {
 
 int launch_write(mjg_ctx *c, int n) {
   const EncGeom &g = c->geom;
-  const int ntasks = g.nchunks * n;
+  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n;
   HIP_TRY(hipMemsetAsync(c->d_status, 0, 4, c->stream));
   tmark(c, MJG_K_WRITE, 0);
   k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
                                        (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status);
-  k_write<<<(ntasks + 3) / 4, 256, 0, c->stream>>>(
+  k_write<<<(ngroups + 3) / 4, 256, 0, c->stream>>>(
       c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
-      c->d_frame_offsets, (int)c->hdr.size(), g.nchunks, ntasks, c->d_out, (uint64_t)c->out_cap);
+      c->d_frame_offsets, (int)c->hdr.size(), g.nchunks, gpf, ngroups, c->d_out, (uint64_t)c->out_cap);
   tmark(c, MJG_K_WRITE, 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->h_sizes, c->d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -471,9 +483,10 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_COUNT_FF, 0);
-  k_count_ff<<<(ntasks + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits,
-                                                          c->d_chunk_off, c->d_frame_bits,
-                                                          c->d_chunk_ff, g.nchunks, ntasks);
+  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
+  k_count_ff<<<(gpf * n + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits, c->d_chunk_off,
+                                                       c->d_frame_bits, c->d_chunk_ff, g.nchunks,
+                                                       gpf, gpf * n);
   tmark(c, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_FF, 0);

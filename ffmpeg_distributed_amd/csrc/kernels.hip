@@ -33,6 +33,30 @@ namespace mjg {
 constexpr int kMaxBlockBits = 1664;  // >= DC 16 + 63 * (16 + 10) bits
 constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 blocks
 
+// fp32 exact-integer arithmetic (k_encode): adding kM = 1.5*2^23 rounds to an integer
+// (round-to-nearest-even) and keeps it in the low mantissa bits; kMb = kM + 32768 leaves
+// value + 32768 in the low 16 bits.  kRnd = 2^-10 turns floor(x/512 + 1/2) into RNE.
+constexpr int kTabWords = 672;  // device table block, see open_ctx
+constexpr float kM = 12582912.0f;
+constexpr float kMb = 12615680.0f;
+constexpr float kRnd = 0x1p-10f;
+
+// jfdctint pass 2 (CONST_BITS 13, PASS1_BITS 4) per output row as one dot product over
+// the 8 column inputs: the LLM butterfly's t/z terms multiplied out (rows 0/4: +-1 with
+// DESCALE 4; others: DESCALE 17).  kPass2Add: rounding constant minus 32768 * row sum
+// (the u16 row image carries +32768).
+__device__ static constexpr int kPass2Dot[64] = {
+    1, 1, 1, 1, 1, 1, 1, 1,
+    11363, 9633, 6437, 2260, -2260, -6437, -9633, -11363,
+    10703, 4433, -4433, -10703, -10703, -4433, 4433, 10703,
+    9633, -2259, -11362, -6436, 6436, 11362, 2259, -9633,
+    1, -1, -1, 1, 1, -1, -1, 1,
+    6437, -11362, 2261, 9633, -9633, -2261, 11362, -6437,
+    4433, -10704, 10704, -4433, -4433, 10704, -10704, 4433,
+    2260, -6436, 9633, -11363, 11363, -9633, 6436, -2260};
+__device__ static constexpr int kPass2Add[8] = {8 - 8 * 32768, 1 << 16, 1 << 16, 1 << 16,
+                                                8, 1 << 16, 1 << 16, 1 << 16};
+
 struct EncGeom {
   int w, h;            // encoded size
   int cw, ch;          // chroma plane size
@@ -185,15 +209,40 @@ struct RegSink {
   }
 };
 
+// Exact quantised coefficient at natural index n of this lane's block, from the row-pass
+// image (pkcol = s_pk + lane: word [r*4 + c/2] holds rows r, columns c, c+1 as u16 = value
+// + 32768).  jfdctint pass 2 for output row ro is one integer dot product over the column
+// (the LLM butterfly's products and sums folded into m2[ro][*]; every partial sum wraps
+// mod 2^32 and the true sum fits int32), then DESCALE and dct_quantize_c's intra rounding:
+// sign(u) * ((|u| * qmat + 3<<18) >> 21), folded into one signed multiply-add.
+__device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const int *m2,
+                                          const int *qc) {
+  const int ro = n >> 3, c = n & 7;
+  const uint32_t sh16 = (uint32_t)(c & 1) << 4;
+  const int4 ma = *(const int4 *)(m2 + ro * 8), mb = *(const int4 *)(m2 + ro * 8 + 4);
+  const int m[8] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
+  int acc = m2[64 + ro];  // rounding constant and the -32768 bias of the u16 image
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int hv = (int)((pkcol[(r * 4 + (c >> 1)) * 64] >> sh16) & 0xffffu);
+    acc = __mul24(hv, m[r]) + acc;
+  }
+  const int u = acc >> (ro == 0 || ro == 4 ? 4 : 17);
+  const int qm = qc[c * 8 + ro];
+  return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
+}
+
 // Bit-pack one block's Huffman codes, FFmpeg mjpegenc.c encode_block /
 // mjpegenc_common.c ff_mjpeg_encode_dc (ZRL 0xF0 per 16 zeros, EOB unless coef 63 != 0).
-// Walks only the nonzero coefficients (64-bit zigzag mask); coefficients come from the
-// wave's LDS block image s_pk[word][lane] (int16 pairs), conflict-free for any per-lane k.
-// (Mean nonzero AC per block is ~1.2 on testsrc2 4K q5, so the loop is short.)
-template <int STRIDE, class Sink>
-__device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask, int diff,
+// `cand` is a superset of the nonzero AC positions in zigzag order (the float screening of
+// the column pass); each candidate is quantised exactly and skipped when it is zero, so
+// runs and EOB are those of the exact block.  (Mean nonzero AC per block is ~1.3 on
+// testsrc2 4K q5, so the loop is short.)
+template <class Sink>
+__device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
                                            const uint32_t *ac, const uint32_t *dc,
-                                           const uint8_t *zz, Sink &sink) {
+                                           const uint8_t *zz, const int *m2, const int *qc,
+                                           Sink &sink) {
   {
     const int cat = dc_cat(diff);
     const uint32_t e = dc[cat];
@@ -201,11 +250,11 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t mask,
     sink.emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);
   }
   int prev = 0;
-  while (mask) {
-    const int k = (int)__builtin_ctzll(mask);
-    mask &= mask - 1;
-    const int n = zz[k];  // natural index of zigzag position k
-    const int v = (int)(int16_t)(pkcol[(n >> 1) * STRIDE] >> (16 * (n & 1)));
+  while (cand) {
+    const int k = (int)__builtin_ctzll(cand);
+    cand &= cand - 1;
+    const int v = exact_coef(pkcol, zz[k], m2, qc);
+    if (v == 0) continue;  // screened in, quantises to zero
     int run = k - prev - 1;
     prev = k;
     while (run >= 16) {
@@ -343,6 +392,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
+  __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
+  __shared__ __attribute__((aligned(16))) int s_m2[72];       // pass-2 dot rows + per-row constant
   __shared__ uint32_t s_win_all[kWavesPerWg][kWaveWinWords];
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
 
@@ -352,7 +403,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
+    s_thr[tid] = __uint_as_float(tabs[608 + tid]);
+    s_m2[tid] = kPass2Dot[tid];
   }
+  if (tid < 8) s_m2[64 + tid] = kPass2Add[tid];
   uint32_t *s_win = s_win_all[wave];
   uint32_t *s_pk = s_pk_all[wave];
   for (int i = lane; i < kWaveWinWords; i += 64) s_win[i] = 0;
@@ -398,23 +452,63 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const int blk = b - 6 * (b / 6);
     const int tab = blk < 4 ? 0 : 1;
     if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, b));
-    // unpack + tv->pc + FDCT row pass, one row at a time; the row outputs (int16 in
-    // FFmpeg, and they fit) go to this wave's LDS block image as pairs [row*4+j][lane].
-    // Luma and chroma share one range formula: chroma's (p*596864 - 9027848) >> 19 ==
-    // (p*2387456 - 36111392) >> 21.
-    const int rmul = tab ? 2387456 : 2441856, radd = tab ? 36111392 : 38008785;
+    // Row pass (jfdctint pass 1) in fp32, exactly: every value is an integer or a multiple
+    // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
+    // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
+    // (M' = 1.5*2^23 + 32768), which also leaves x + 32768 in the low 16 mantissa bits:
+    // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
+    // [RC] swscale tv->pc per pixel: fma + round-to-integer via + M (M = 1.5*2^23) + clamp
+    // with med3 reproduces clip_u8((p * A21 - B21) >> 21) for all 256 p (checked
+    // exhaustively in tests/test_oracle.py); values then carry the +M bias, which the
+    // butterfly's differences cancel and its sums remove with one -2M.
+    const float rA = tab ? 0x1.237p+0f : 0x1.2a14p+0f;        // 2387456 / 2^21, 2441856 / 2^21
+    const float rB = tab ? -0x1.1b821p+4f : -0x1.29fbe8p+4f;  // -17.719253..., -18.624000...
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-      int cr[8];
+      const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
+      float p[8];
+      p[0] = (float)((lo >> 0) & 255u);  // v_cvt_f32_ubyte0
+      p[1] = (float)((lo >> 8) & 255u);  // v_cvt_f32_ubyte1
+      p[2] = (float)((lo >> 16) & 255u);  // v_cvt_f32_ubyte2
+      p[3] = (float)((lo >> 24) & 255u);  // v_cvt_f32_ubyte3
+      p[4] = (float)((hi >> 0) & 255u);  // v_cvt_f32_ubyte0
+      p[5] = (float)((hi >> 8) & 255u);  // v_cvt_f32_ubyte1
+      p[6] = (float)((hi >> 16) & 255u);  // v_cvt_f32_ubyte2
+      p[7] = (float)((hi >> 24) & 255u);  // v_cvt_f32_ubyte3
+      float t0, t1, t2, t3;
+      if (rc) {
 #pragma unroll
-      for (int x = 0; x < 8; x++) {
-        const int p = (int)((raw[r] >> (8 * x)) & 255u);
-        cr[x] = !rc ? p : min(max((__mul24(p, rmul) - radd) >> 21, 0), 255);
+        for (int x = 0; x < 8; x++)
+          p[x] = __builtin_amdgcn_fmed3f(__builtin_fmaf(p[x], rA, rB) + kM, kM, kM + 255.0f);
+        t0 = (p[0] - 2.0f * kM) + p[7];
+        t1 = (p[1] - 2.0f * kM) + p[6];
+        t2 = (p[2] - 2.0f * kM) + p[5];
+        t3 = (p[3] - 2.0f * kM) + p[4];
+      } else {
+        t0 = p[0] + p[7];
+        t1 = p[1] + p[6];
+        t2 = p[2] + p[5];
+        t3 = p[3] + p[4];
       }
-      fdct8<1, true>(cr);
+      const float t7 = p[0] - p[7], t6 = p[1] - p[6], t5 = p[2] - p[5], t4 = p[3] - p[4];
+      const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+      float o[8];
+      o[0] = __builtin_fmaf(t10 + t11, 16.0f, kMb);
+      o[4] = __builtin_fmaf(t10 - t11, 16.0f, kMb);
+      o[2] = __builtin_fmaf(t13, 10703.0f / 512, __builtin_fmaf(t12, 4433.0f / 512, kRnd)) + kMb;
+      o[6] = __builtin_fmaf(t13, 4433.0f / 512, __builtin_fmaf(t12, -10704.0f / 512, kRnd)) + kMb;
+      o[1] = __builtin_fmaf(t7, 11363.0f / 512, __builtin_fmaf(t6, 9633.0f / 512,
+             __builtin_fmaf(t5, 6437.0f / 512, __builtin_fmaf(t4, 2260.0f / 512, kRnd)))) + kMb;
+      o[3] = __builtin_fmaf(t7, 9633.0f / 512, __builtin_fmaf(t6, -2259.0f / 512,
+             __builtin_fmaf(t5, -11362.0f / 512, __builtin_fmaf(t4, -6436.0f / 512, kRnd)))) + kMb;
+      o[5] = __builtin_fmaf(t7, 6437.0f / 512, __builtin_fmaf(t6, -11362.0f / 512,
+             __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMb;
+      o[7] = __builtin_fmaf(t7, 2260.0f / 512, __builtin_fmaf(t6, -6436.0f / 512,
+             __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMb;
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        s_pk[(r * 4 + j) * 64 + lane] = ((uint32_t)cr[2 * j] & 0xffffu) | ((uint32_t)cr[2 * j + 1] << 16);
+        s_pk[(r * 4 + j) * 64 + lane] =
+            __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
       __builtin_amdgcn_sched_barrier(0);
     }
     // prefetch the next chunk while this one is encoded
@@ -436,59 +530,69 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
     const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, chunk, lane) : 0;
 
-    // Column pass two columns at a time from the LDS row image, each coefficient
-    // quantised straight into a packed zigzag register image (qpk), which then replaces
-    // the consumed row image.  dct_quantize_c (intra, MJPEG): DC (c+32)/64; AC
-    // sign(c) * ((|c|*qmat + 3<<18) >> 21), folded into one signed multiply-add:
-    // (c*qmat + (c < 0 ? 2^21-1-(3<<18) : 3<<18)) >> 21.  clip_coeffs (+-1023) never
-    // fires: |AC| <= ~6710 for 8-bit input, so |q| <= 419 even at qscale 1.
+    // Column pass (jfdctint pass 2) as a float *screen*: the products of pass 2 need up to
+    // 31 bits, so fp32 sums are only approximate (|error| < 2^9 before the 2^17 descale).
+    // Each AC coefficient is tested against its quantiser threshold widened by a margin
+    // (s_thr = B^2, fma(-s, s, B^2) < 0 <=> |s| > B), giving a candidate mask in zigzag
+    // order; emit_block quantises the candidates exactly from the integer row image
+    // (exact_coef).  Rows 0 and 4 (sums only) are exact, which gives the DC exactly:
+    // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
     int dc = 0;
     uint32_t mlo = 0, mhi = 0;
     if (cur_active) {
 #pragma unroll
       for (int jp = 0; jp < 4; jp++) {
         __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
-        int cc[2][8];
+        uint32_t w[8];
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-          const uint32_t w = s_pk[(r * 4 + jp) * 64 + lane];
-          cc[0][r] = (int)(int16_t)(w & 0xffffu);
-          cc[1][r] = (int)(int16_t)(w >> 16);
-        }
+        for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           __builtin_amdgcn_sched_barrier(0);  // one column at a time
           const int col = 2 * jp + h;
-          fdct8<1, false>(cc[h]);
-          const int4 qa = *(const int4 *)(s_qc + col * 8), qb = *(const int4 *)(s_qc + col * 8 + 4);
-          const int qm[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+          float x[8];
+#pragma unroll
+          for (int r = 0; r < 8; r++)
+            x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));
+          // x = M' + value: differences cancel the bias, sums drop it with one -2M'
+          const float t0 = (x[0] - 2.0f * kMb) + x[7], t7 = x[0] - x[7];
+          const float t1 = (x[1] - 2.0f * kMb) + x[6], t6 = x[1] - x[6];
+          const float t2 = (x[2] - 2.0f * kMb) + x[5], t5 = x[2] - x[5];
+          const float t3 = (x[3] - 2.0f * kMb) + x[4], t4 = x[3] - x[4];
+          const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+          float sv[8];
+          sv[0] = t10 + t11;
+          sv[4] = t10 - t11;
+          sv[2] = __builtin_fmaf(t13, 10703.0f, t12 * 4433.0f);
+          sv[6] = __builtin_fmaf(t13, 4433.0f, t12 * -10704.0f);
+          sv[1] = __builtin_fmaf(t7, 11363.0f, __builtin_fmaf(t6, 9633.0f, __builtin_fmaf(t5, 6437.0f, t4 * 2260.0f)));
+          sv[3] = __builtin_fmaf(t7, 9633.0f, __builtin_fmaf(t6, -2259.0f, __builtin_fmaf(t5, -11362.0f, t4 * -6436.0f)));
+          sv[5] = __builtin_fmaf(t7, 6437.0f, __builtin_fmaf(t6, -11362.0f, __builtin_fmaf(t5, 2261.0f, t4 * 9633.0f)));
+          sv[7] = __builtin_fmaf(t7, 2260.0f, __builtin_fmaf(t6, -6436.0f, __builtin_fmaf(t5, 9633.0f, t4 * -11363.0f)));
+          const float4 ta = *(const float4 *)(s_thr + col * 8), tb = *(const float4 *)(s_thr + col * 8 + 4);
+          const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
 #pragma unroll
           for (int r = 0; r < 8; r++) {
             const int k = kZigzagInv[r * 8 + col];
-            const int x = cc[h][r];
-            int v;
             if (k == 0) {
-              dc = (x + 32) >> 6;
-              v = dc;
+              dc = (int)(__float_as_uint(__builtin_fmaf(sv[0], 1.0f / 1024, 0x1.1p-7f) + kM) - 0x4B400000u);
             } else {
-              v = (__mul24(x, qm[r]) + (x < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
-              const uint32_t nz = min((uint32_t)v, 1u);
+              const uint32_t neg = __float_as_uint(__builtin_fmaf(-sv[r], sv[r], thr[r]));
               if (k < 32)
-                mlo |= nz << k;
+                mlo |= (neg >> (31 - k)) & (1u << k);
               else
-                mhi |= nz << (k - 32);
+                mhi |= (neg >> (63 - k)) & (1u << (k - 32));
             }
-            cc[h][r] = v;
           }
         }
-        // quantised pair (row r, columns 2jp, 2jp+1) replaces the row-pass pair it came
-        // from: the block image is now the quantised block in natural order
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-          const uint32_t w = ((uint32_t)cc[0][r] & 0xffffu) | ((uint32_t)cc[1][r] << 16);
-          s_pk[(r * 4 + jp) * 64 + lane] = w;
-          if (g.debug_coefs)  // natural-order int16 pairs
-            ((uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64))[r * 4 + jp] = w;
+      }
+      if (g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
+        uint32_t *dst = (uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64);
+#pragma unroll 1
+        for (int n = 0; n < 64; n += 2) {
+          const int a0 = n == 0 ? dc : exact_coef(s_pk + lane, n, s_m2, s_qc);
+          const int a1 = exact_coef(s_pk + lane, n + 1, s_m2, s_qc);
+          dst[n >> 1] = ((uint32_t)a0 & 0xffffu) | ((uint32_t)a1 << 16);
         }
       }
     }
@@ -506,7 +610,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     RegSink q;
 #if MJG_ABLATE == 0
     if (cur_active) {
-      emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, q);
+      emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, q);
       q.finish();
     }
 #else
@@ -545,7 +649,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
           sink.wbase = wbase;
           sink.win = s_win;
           sink.cap = kWaveWinWords;
-          emit_block<64>(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, sink);
+          emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, sink);
           sink.finish();
         }
       }
@@ -656,26 +760,35 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
-// Wave per chunk (4 per workgroup), lane = word: realign the chunk's words to its frame
-// offset and count the 0xFF bytes among the bytes it owns (a byte belongs to the chunk
-// holding its first bit).
+// Wave per run of kChunksPerWave chunks of one frame (4 waves per workgroup), lane = word:
+// realign each chunk's words to its frame offset and count the 0xFF bytes among the bytes
+// it owns (a byte belongs to the chunk holding its first bit).  A chunk is ~27 words at
+// 4K q5, so one chunk per wave left the launch dominated by wave start-up.
+constexpr int kChunksPerWave = 8;
+
 __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
                                                   const uint32_t *__restrict__ chunk_bits,
                                                   const uint32_t *__restrict__ chunk_off,
                                                   const uint32_t *__restrict__ frame_bits,
                                                   uint32_t *__restrict__ chunk_ff, int nchunks,
-                                                  int ntotal) {
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (i >= ntotal) return;
-  const int f = i / nchunks, c = i - f * nchunks;
-  const uint32_t O = chunk_off[i], L = chunk_bits[i], T = frame_bits[f];
+                                                  int ngroups_per_frame, int ngroups) {
+  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (gi >= ngroups) return;
+  const int f = gi / ngroups_per_frame;
+  const int c0 = (gi - f * ngroups_per_frame) * kChunksPerWave;
+  const int c1 = min(c0 + kChunksPerWave, nchunks);
+  const uint32_t T = frame_bits[f];
   const uint32_t total_bytes = (T + 7) >> 3;
-  const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-  int cnt = 0;
-  for (uint32_t k = k0 + lane; k < k1; k += 64)
-    cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k), 4 * k, total_bytes);
-  cnt = wave_sum(cnt);
-  if (lane == 0) chunk_ff[i] = (uint32_t)cnt;
+  for (int c = c0; c < c1; c++) {
+    const int i = f * nchunks + c;
+    const uint32_t O = chunk_off[i], L = chunk_bits[i];
+    const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
+    int cnt = 0;
+    for (uint32_t k = k0 + lane; k < k1; k += 64)
+      cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k), 4 * k, total_bytes);
+    cnt = wave_sum(cnt);
+    if (lane == 0) chunk_ff[i] = (uint32_t)cnt;
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ chunk_ff,
@@ -718,45 +831,51 @@ __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ f
   }
 }
 
-// Wave per chunk, lane = word: the chunk's owned bytes with a 0x00 after every 0xFF
-// (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs before it in the
-// frame (chunk prefix from k_scan_ff, in-chunk prefix by a wave scan).
+// Wave per run of kChunksPerWave chunks, lane = word: each chunk's owned bytes with a
+// 0x00 after every 0xFF (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs
+// before it in the frame (chunk prefix from k_scan_ff, in-chunk prefix by a wave scan).
 __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
     const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
     const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
-    const uint64_t *__restrict__ frame_offsets, int hdr_len, int nchunks, int ntotal,
-    uint8_t *__restrict__ out, uint64_t out_cap) {
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (i >= ntotal) return;
-  const int f = i / nchunks, c = i - f * nchunks;
+    const uint64_t *__restrict__ frame_offsets, int hdr_len, int nchunks, int ngroups_per_frame,
+    int ngroups, uint8_t *__restrict__ out, uint64_t out_cap) {
+  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (gi >= ngroups) return;
+  const int f = gi / ngroups_per_frame;
+  const int c0 = (gi - f * ngroups_per_frame) * kChunksPerWave;
+  const int c1 = min(c0 + kChunksPerWave, nchunks);
   const uint64_t foff = frame_offsets[f];
   if (foff + frame_size[f] > out_cap) return;  // k_frame_hdr flagged the overflow
-  const uint32_t O = chunk_off[i], L = chunk_bits[i], T = frame_bits[f];
+  const uint32_t T = frame_bits[f];
   const uint32_t total_bytes = (T + 7) >> 3;
-  const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-  uint8_t *base = out + foff + hdr_len + 4 * (size_t)k0 + ff_off[i];
-  uint32_t carry = 0;
-  for (uint32_t kb = k0; kb < k1; kb += 64) {
-    const uint32_t k = kb + lane;
-    uint32_t v = 0, cnt = 0;
-    if (k < k1) {
-      v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
-      cnt = (uint32_t)ff_in_word(v, 4 * k, total_bytes);
-    }
-    const uint32_t incl = wave_incl_scan(cnt, lane);
-    if (k < k1) {
-      uint8_t *p = base + 4 * (k - k0) + carry + incl - cnt;
+  for (int c = c0; c < c1; c++) {
+    const int i = f * nchunks + c;
+    const uint32_t O = chunk_off[i], L = chunk_bits[i];
+    const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
+    uint8_t *base = out + foff + hdr_len + 4 * (size_t)k0 + ff_off[i];
+    uint32_t carry = 0;
+    for (uint32_t kb = k0; kb < k1; kb += 64) {
+      const uint32_t k = kb + lane;
+      uint32_t v = 0, cnt = 0;
+      if (k < k1) {
+        v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
+        cnt = (uint32_t)ff_in_word(v, 4 * k, total_bytes);
+      }
+      const uint32_t incl = wave_incl_scan(cnt, lane);
+      if (k < k1) {
+        uint8_t *p = base + 4 * (k - k0) + carry + incl - cnt;
 #pragma unroll
-      for (int bb = 0; bb < 4; bb++) {
-        if (4 * k + bb < total_bytes) {
-          const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
-          *p++ = byte;
-          if (byte == 0xff) *p++ = 0;
+        for (int bb = 0; bb < 4; bb++) {
+          if (4 * k + bb < total_bytes) {
+            const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
+            *p++ = byte;
+            if (byte == 0xff) *p++ = 0;
+          }
         }
       }
+      carry += __shfl(incl, 63, 64);
     }
-    carry += __shfl(incl, 63, 64);
   }
 }
 

@@ -1,0 +1,187 @@
+"""CPU proofs for the fp32 exact-integer arithmetic of k_encode (csrc/kernels.hip).
+
+The kernel carries jfdctint's integer pass 1 in fp32 mantissas and uses fp32 only as a
+*screen* in pass 2 (exact values come from integer dot products).  These tests restate
+those steps in numpy (fp32 FMA = exact float64 product-sum rounded once to fp32) and pin
+them against the C oracle's FDCT (oracle/mjpeg_oracle.c, a restatement of FFmpeg's
+jfdctint_template.c) and swscale's range converters:
+  - the fp32 tv->pc range conversion equals the integer formula for all 256 inputs,
+  - the fp32 row pass equals jfdctint pass 1 for random and extreme rows,
+  - kPass2Dot/kPass2Add (pass 2 as one dot product per output row) equal the oracle FDCT,
+  - the screening thresholds never drop a coefficient that quantises to nonzero.
+Constants are parsed from the kernel source so the test cannot drift from it.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+
+SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "ffmpeg_distributed_amd", "csrc", "kernels.hip")
+M = np.float32(12582912.0)
+MB = np.float32(12615680.0)
+RND = np.float32(2.0 ** -10)
+
+
+def _src():
+    with open(SRC) as f:
+        return f.read()
+
+
+def _int_array(name):
+    body = re.search(name + r"\[\d+\]\s*=\s*\{([^}]*)\}", _src()).group(1)
+    return [int(eval(x)) for x in body.replace("\n", " ").split(",") if x.strip()]
+
+
+def _hexfloats():
+    s = _src()
+    a = re.search(r"const float rA = tab \? ([^ ]+) : ([^;]+);", s)
+    b = re.search(r"const float rB = tab \? ([^ ]+) : ([^;]+);", s)
+    f = lambda t: np.float32(float.fromhex(t.strip().rstrip("f")))
+    return {"C": (f(a.group(1)), f(b.group(1))), "Y": (f(a.group(2)), f(b.group(2)))}
+
+
+def fma32(a, b, c):
+    """fp32 fused multiply-add: exact in float64 for these magnitudes, one rounding."""
+    return (np.float64(np.float32(a)) * np.float64(np.float32(b)) + np.float64(np.float32(c))).astype(np.float32)
+
+
+def range_int(p, chroma):
+    if chroma:
+        return np.clip((p * 2387456 - 36111392) >> 21, 0, 255)
+    return np.clip((p * 2441856 - 38008785) >> 21, 0, 255)
+
+
+def range_f32(p, chroma):
+    A, B = _hexfloats()["C" if chroma else "Y"]
+    r = (fma32(p.astype(np.float32), A, B) + M).astype(np.float32)
+    return np.minimum(np.maximum(r, M), (M + np.float32(255)).astype(np.float32))  # med3
+
+
+@pytest.mark.parametrize("chroma", [False, True])
+def test_fp32_range_convert_exhaustive(chroma):
+    p = np.arange(256, dtype=np.int64)
+    got = (range_f32(p, chroma).astype(np.float64) - float(M)).astype(np.int64)
+    assert (got == range_int(p, chroma)).all()
+
+
+def pass1_int(p):
+    """jfdctint pass 1 (CONST_BITS 13, PASS1_BITS 4) on rows of 8, int64."""
+    D = lambda x, n: (x + (1 << (n - 1))) >> n
+    p = p.astype(np.int64)
+    t0, t7 = p[:, 0] + p[:, 7], p[:, 0] - p[:, 7]
+    t1, t6 = p[:, 1] + p[:, 6], p[:, 1] - p[:, 6]
+    t2, t5 = p[:, 2] + p[:, 5], p[:, 2] - p[:, 5]
+    t3, t4 = p[:, 3] + p[:, 4], p[:, 3] - p[:, 4]
+    t10, t13, t11, t12 = t0 + t3, t0 - t3, t1 + t2, t1 - t2
+    o = np.zeros_like(p)
+    o[:, 0] = (t10 + t11) * 16
+    o[:, 4] = (t10 - t11) * 16
+    z1 = (t12 + t13) * 4433
+    o[:, 2] = D(z1 + t13 * 6270, 9)
+    o[:, 6] = D(z1 - t12 * 15137, 9)
+    z1, z2, z3, z4 = t4 + t7, t5 + t6, t4 + t6, t5 + t7
+    z5 = (z3 + z4) * 9633
+    t4, t5, t6, t7 = t4 * 2446, t5 * 16819, t6 * 25172, t7 * 12299
+    z1, z2, z3, z4 = z1 * -7373, z2 * -20995, z3 * -16069 + z5, z4 * -3196 + z5
+    o[:, 7] = D(t4 + z1 + z3, 9)
+    o[:, 5] = D(t5 + z2 + z4, 9)
+    o[:, 3] = D(t6 + z2 + z3, 9)
+    o[:, 1] = D(t7 + z1 + z4, 9)
+    return o
+
+
+def pass1_f32(p, rc_chroma=None):
+    """The kernel's fp32 row pass; returns the u16 image values (value + 32768)."""
+    f = lambda a: np.asarray(a, np.float32)
+    if rc_chroma is None:
+        x = [f(p[:, i]) for i in range(8)]
+        t0, t1, t2, t3 = (f(x[0] + x[7]), f(x[1] + x[6]), f(x[2] + x[5]), f(x[3] + x[4]))
+    else:
+        x = [range_f32(p[:, i].astype(np.int64), rc_chroma) for i in range(8)]
+        t0 = f(f(x[0] - f(2 * M)) + x[7])
+        t1 = f(f(x[1] - f(2 * M)) + x[6])
+        t2 = f(f(x[2] - f(2 * M)) + x[5])
+        t3 = f(f(x[3] - f(2 * M)) + x[4])
+    t7, t6, t5, t4 = f(x[0] - x[7]), f(x[1] - x[6]), f(x[2] - x[5]), f(x[3] - x[4])
+    t10, t13, t11, t12 = f(t0 + t3), f(t0 - t3), f(t1 + t2), f(t1 - t2)
+    c = lambda v: np.float32(v / 512)
+    o = [None] * 8
+    o[0] = fma32(f(t10 + t11), 16.0, MB)
+    o[4] = fma32(f(t10 - t11), 16.0, MB)
+    o[2] = f(fma32(t13, c(10703), fma32(t12, c(4433), RND)) + MB)
+    o[6] = f(fma32(t13, c(4433), fma32(t12, c(-10704), RND)) + MB)
+    odd = {1: (2260, 6437, 9633, 11363), 3: (-6436, -11362, -2259, 9633),
+           5: (9633, 2261, -11362, 6437), 7: (-11363, 9633, -6436, 2260)}
+    for k, (c4, c5, c6, c7) in odd.items():
+        a = fma32(t4, c(c4), RND)
+        a = fma32(t5, c(c5), a)
+        a = fma32(t6, c(c6), a)
+        a = fma32(t7, c(c7), a)
+        o[k] = f(a + MB)
+    bits = np.stack([v.view(np.uint32) for v in o], 1)
+    return (bits & 0xFFFF).astype(np.int64)
+
+
+def _rows(rng, n):
+    r = rng.integers(0, 256, (n, 8))
+    r[: n // 4] = rng.choice([0, 255], (n // 4, 8))  # extremes stress the magnitudes
+    r[n // 4: n // 4 + 2] = [[0, 255] * 4, [255, 0] * 4]
+    return r
+
+
+def test_fp32_row_pass_equals_jfdctint_pass1():
+    rng = np.random.default_rng(1)
+    p = _rows(rng, 200000)
+    assert (pass1_f32(p) - 32768 == pass1_int(p)).all()
+
+
+@pytest.mark.parametrize("chroma", [False, True])
+def test_fp32_row_pass_with_range_convert(chroma):
+    rng = np.random.default_rng(2 + chroma)
+    p = _rows(rng, 100000)
+    ref = pass1_int(range_int(p.astype(np.int64), chroma))
+    assert (pass1_f32(p, rc_chroma=chroma) - 32768 == ref).all()
+
+
+def test_pass2_dot_rows_equal_oracle_fdct():
+    dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
+    add = np.array(_int_array("kPass2Add"), np.int64)
+    sh = np.array([4, 17, 17, 17, 4, 17, 17, 17])
+    rng = np.random.default_rng(3)
+    for it in range(300):
+        blk = rng.integers(0, 256, (8, 8)) if it % 3 else rng.choice([0, 255], (8, 8))
+        ref = oracle.fdct(blk.astype(np.int16)).reshape(8, 8).astype(np.int64)
+        img = pass1_f32(blk)  # rows -> u16 image (value + 32768), [row][col]
+        for c in range(8):
+            col = img[:, c]
+            acc = (dot @ col + add).astype(np.int64)
+            acc = ((acc + 2 ** 31) % 2 ** 32) - 2 ** 31  # int32 wraparound, as on the GPU
+            assert ((acc >> sh) == ref[:, c]).all(), (it, c)
+
+
+def test_screen_thresholds_are_conservative():
+    """Every coefficient that quantises to nonzero passes the fp32 screen (q = 1..31)."""
+    dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
+    rng = np.random.default_rng(4)
+    blocks = rng.integers(0, 256, (400, 8, 8))
+    blocks[:100] = rng.choice([0, 255], (100, 8, 8))
+    for q in (1, 2, 5, 13, 31):
+        qm = oracle.matrix(q)[1].astype(np.int64)  # natural order
+        T = ((5 << 18) + qm - 1) // qm
+        for blk in blocks:
+            img = pass1_f32(blk)
+            coefs = oracle.quantize(oracle.fdct(blk.astype(np.int16)), q)[0].reshape(8, 8)
+            for c in range(8):
+                s_exact = dot @ (img[:, c] - 32768)
+                for r in range(8):
+                    n = r * 8 + c
+                    if n == 0 or coefs[r, c] == 0:
+                        continue
+                    B = 16.0 * T[n] - 8.5 if r in (0, 4) else T[n] * 131072.0 - 65536.0 - 2048.0
+                    # the kernel's fp32 sum differs from s_exact by < 2^9 (see kernels.hip)
+                    slack = 0 if r in (0, 4) else 512  # rows 0/4 are exact in fp32
+                    assert abs(s_exact[r]) - slack > B, (q, n, s_exact[r], B)

@@ -113,6 +113,126 @@ K(k40, T40)
 #define T41(i) "v_cvt_pk_i16_i32 %" #i ", %8, %" #i "\n"
 K(k41, T41)
 
+#define T42(i) "v_cvt_flr_i32_f32 %" #i ", %" #i "\n"
+K(k42, T42)
+#define T43(i) "v_cvt_i32_f32 %" #i ", %" #i "\n"
+K(k43, T43)
+#define T44(i) "v_floor_f32 %" #i ", %" #i "\n"
+K(k44, T44)
+#define T45(i) "v_med3_f32 %" #i ", %" #i ", %8, %9\n"
+K(k45, T45)
+#define T46(i) "v_add_f32 %" #i ", %8, %" #i "\n"
+K(k46, T46)
+#define T47(i) "v_mul_f32 %" #i ", %8, %" #i "\n"
+K(k47, T47)
+#define T48(i) "v_cvt_f32_i32 %" #i ", %" #i "\n"
+K(k48, T48)
+#define T49(i) "v_pk_sub_u16 %" #i ", %8, %" #i " clamp\n"
+K(k49, T49)
+#define T50(i) "v_pk_lshrrev_b16 %" #i ", 3, %" #i "\n"
+K(k50, T50)
+#define T51(i) "v_sub_co_u32 %" #i ", vcc, %8, %" #i "\n"
+K(k51, T51)
+#define T52(i) "v_addc_co_u32 %" #i ", vcc, %" #i ", %" #i ", vcc\n"
+K(k52, T52)
+#define T53(i) "v_mul_hi_u32 %" #i ", %8, %" #i "\n"
+K(k53, T53)
+#define T54(i) "v_max3_i32 %" #i ", %8, %9, %" #i "\n"
+K(k54, T54)
+#define T55(i) "v_mad_u32_u16 %" #i ", %8, %9, %" #i "\n"
+K(k55, T55)
+#define T56(i) "v_cvt_f32_ubyte0_sdwa %" #i ", %8 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD\n"
+K(k56, T56)
+
+#define T57(i) "v_cmp_gt_i32 vcc, %8, %" #i "\nv_cndmask_b32 %" #i ", %8, %" #i ", vcc\n"
+K(k57, T57)
+#define T58(i) "v_cmp_gt_i32 vcc, %8, %" #i "\n"
+K(k58, T58)
+#define T59(i) "v_cndmask_b32_e64 %" #i ", %8, %" #i ", s[20:21]\n"
+K(k59, T59)
+#define T60(i) "v_cmp_gt_i32 s[20:21], %8, %" #i "\nv_cndmask_b32_e64 %" #i ", %8, %" #i ", s[20:21]\n"
+K(k60, T60)
+#define T61(i) "v_sad_u32 %" #i ", %8, %9, %" #i "\n"
+K(k61, T61)
+#define T62(i) "v_max_f32 %" #i ", %8, %" #i "\n"
+K(k62, T62)
+#define T63(i) "v_subrev_u32 %" #i ", %8, %" #i "\n"
+K(k63, T63)
+#define T64(i) "v_sub_f32 %" #i ", %8, %" #i "\n"
+K(k64, T64)
+#define T65(i) "v_add_u32 %" #i ", 0x4b400000, %" #i "\n"
+K(k65, T65)
+#define T67(i) "v_mul_f32 %" #i ", 0x3f800001, %" #i "\n"
+K(k67, T67)
+#define T68(i) "v_add_f32 %" #i ", 0x4b400000, %" #i "\n"
+K(k68, T68)
+#define T70(i) "v_bitop3_b32 %" #i ", %8, %9, %" #i " bitop3:0xf8\n"
+K(k70, T70)
+#define T71(i) "v_lshl_add_u64 %" #i ", %8, 0, %" #i "\n"
+#define T69(i) "v_add_u32 %" #i ", %" #i ", %" #i "\n"
+K(k69, T69)
+
+// LDS LUT lookup throughput: 256-byte table, per-lane random byte index (conflict-free)
+__global__ void lut_u8(int *out, int seed) {
+  __shared__ unsigned char lut[256];
+  __shared__ float flut[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) { lut[i] = (unsigned char)(i * 7); flut[i] = i; }
+  __syncthreads();
+  unsigned a[8];
+  for (int j = 0; j < 8; j++) a[j] = (seed + threadIdx.x * 13 + j * 29) & 255;
+  for (int i = 0; i < ITERS; i++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) a[j] = lut[a[j]];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7];
+}
+__global__ void lut_f32(int *out, int seed) {
+  __shared__ float flut[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) flut[i] = (float)((i * 7) & 255);
+  __syncthreads();
+  unsigned a[8];
+  for (int j = 0; j < 8; j++) a[j] = (seed + threadIdx.x * 13 + j * 29) & 255;
+  for (int i = 0; i < ITERS; i++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) a[j] = (unsigned)flut[a[j]];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7];
+}
+
+// 64-bit (register-pair) chains for packed fp32 and 64-bit shifts
+#define K64(NAME, TEMPLATE)                                                                \
+  __global__ void NAME(int *out, int seed) {                                               \
+    long long a0 = seed + threadIdx.x, a1 = a0 ^ 3, a2 = a0 * 5, a3 = a0 + 7, a4 = a0 ^ 11,\
+        a5 = a0 * 13, a6 = a0 + 17, a7 = a0 ^ 19;                                          \
+    long long x = seed * 3 + 1, y = seed ^ 0x55;                                           \
+    for (int i = 0; i < ITERS; i++) {                                                      \
+      asm volatile(TEMPLATE(0) TEMPLATE(1) TEMPLATE(2) TEMPLATE(3) TEMPLATE(4) TEMPLATE(5) \
+                       TEMPLATE(6) TEMPLATE(7)                                             \
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), \
+                     "+v"(a7)                                                              \
+                   : "v"(x), "v"(y));                                                      \
+    }                                                                                      \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (int)(a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7); \
+  }
+#define P0(i) "v_pk_fma_f32 %" #i ", %8, %9, %" #i "\n"
+K64(q0, P0)
+#define P1(i) "v_pk_add_f32 %" #i ", %8, %" #i "\n"
+K64(q1, P1)
+#define P2(i) "v_pk_mul_f32 %" #i ", %8, %" #i "\n"
+K64(q2, P2)
+#define P3(i) "v_lshlrev_b64 %" #i ", 3, %" #i "\n"
+K64(q3, P3)
+#define P4(i) "v_pk_mov_b32 %" #i ", %8, %" #i " op_sel:[1,0]\n"
+K64(q4, P4)
+
+// clamp semantics of v_pk_mad_i16: is the saturation applied to the full product?
+__global__ void clamp_probe(int *out) {
+  int r;
+  const int a = (200 << 16) | 255, b = (149 << 16) | 149, c = (0xffff & -1000) | ((0xffff & -1000) << 16);
+  asm volatile("v_pk_mad_i16 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  if (threadIdx.x == 0) out[0] = r;
+}
+
 typedef void (*kfn)(int *, int);
 
 int main() {
@@ -168,7 +288,42 @@ int main() {
 {"v_cvt_f32_ubyte1", k38},
 {"v_fmac_f32", k39},
 {"v_fma_f32", k40},
-{"v_cvt_pk_i16_i32", k41}};
+{"v_cvt_pk_i16_i32", k41},
+{"v_cvt_flr_i32_f32", k42},
+{"v_cvt_i32_f32", k43},
+{"v_floor_f32", k44},
+{"v_med3_f32", k45},
+{"v_add_f32", k46},
+{"v_mul_f32", k47},
+{"v_cvt_f32_i32", k48},
+{"v_pk_sub_u16_clamp", k49},
+{"v_pk_lshrrev_b16", k50},
+{"v_sub_co_u32", k51},
+{"v_addc_co_u32", k52},
+{"v_mul_hi_u32", k53},
+{"v_max3_i32", k54},
+{"v_mad_u32_u16", k55},
+{"v_cvt_f32_ubyte0_sdwa", k56},
+{"cmp+cndmask(vcc) pair", k57},
+{"v_cmp_gt_i32 (vcc)", k58},
+{"v_cndmask_e64 s[20:21]", k59},
+{"cmp+cndmask(s pair)", k60},
+{"v_sad_u32", k61},
+{"v_max_f32", k62},
+{"v_subrev_u32", k63},
+{"v_sub_f32", k64},
+{"v_add_u32 literal", k65},
+{"v_mul_f32 literal", k67},
+{"v_add_f32 literal", k68},
+{"v_add_u32 x+x", k69},
+{"v_bitop3_b32", k70},
+{"lds lut u8 (per lookup)", lut_u8},
+{"lds lut f32 (per lookup, +cvt)", lut_f32},
+{"v_pk_fma_f32", q0},
+{"v_pk_add_f32", q1},
+{"v_pk_mul_f32", q2},
+{"v_lshlrev_b64", q3},
+{"v_pk_mov_b32", q4}};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -188,5 +343,10 @@ int main() {
     printf("%-18s %8.3f ms  %.3f wave-instr/ns/SIMD  (%.2f cyc @2.4GHz)\n", k.name, ms,
            per_simd / ns, 2.4 * ns / per_simd);
   }
+  hipLaunchKernelGGL(clamp_probe, dim3(1), dim3(64), 0, 0, out);
+  int r = 0;
+  (void)hipMemcpy(&r, out, 4, hipMemcpyDeviceToHost);
+  printf("v_pk_mad_i16 clamp probe: lo %d (255*149-1000=%d) hi %d (200*149-1000=%d)\n", (short)(r & 0xffff),
+         255 * 149 - 1000, (short)(r >> 16), 200 * 149 - 1000);
   return 0;
 }
