@@ -27,7 +27,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # -fno-slp-vectorize: the SLP vectoriser packs k_encode's per-column fp32 chains into
+    # v_pk_fma_f32 across columns, which doubles live registers (123 VGPRs -> 168 + 180 B
+    # of scratch spills per lane) and costs ~30% of k_encode time.
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:

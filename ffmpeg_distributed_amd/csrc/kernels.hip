@@ -25,7 +25,7 @@
 #define MJG_ENC_WAVES_PER_EU 3  // k_encode occupancy target (waves per SIMD); measured best (v8)
 #endif
 #ifndef MJG_ABLATE
-#define MJG_ABLATE 0  // perf experiments only: 1 = no bit-pack
+#define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store
 #endif
 
 namespace mjg {
@@ -54,6 +54,14 @@ __device__ static constexpr int kPass2Dot[64] = {
     6437, -11362, 2261, 9633, -9633, -2261, 11362, -6437,
     4433, -10704, 10704, -4433, -4433, 10704, -10704, 4433,
     2260, -6436, 9633, -11363, 11363, -9633, 6436, -2260};
+// k_encode screen bit -> zigzag scan position.  Columns 0-3 (DC excluded) are shifted
+// into word A in the order col-major (col, row), columns 4-7 into word B, so the j-th
+// coefficient screened lands at bit 30-j (A) / 31-j (B).
+__device__ static constexpr uint8_t kScreenScatter[64] = {
+    49, 47, 38, 32, 24, 17, 13, 6, 48, 37, 33, 23, 18, 12, 7, 5,
+    36, 34, 22, 19, 11, 8, 4, 1, 35, 21, 20, 10, 9, 3, 2, 0,
+    63, 61, 60, 54, 53, 43, 42, 28, 62, 59, 55, 52, 44, 41, 29, 27,
+    58, 56, 51, 45, 40, 30, 26, 15, 57, 50, 46, 39, 31, 25, 16, 14};
 __device__ static constexpr int kPass2Add[8] = {8 - 8 * 32768, 1 << 16, 1 << 16, 1 << 16,
                                                 8, 1 << 16, 1 << 16, 1 << 16};
 
@@ -146,16 +154,23 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
-struct BitSink {
+// Second emission pass of a block longer than RegSink's 4 words: bits at the block's
+// chunk offset, interior words stored to the slot, first/last word kept for the opener
+// logic of the pack step (k_encode).
+struct SlotSink {
   uint64_t acc;
-  int nacc;        // bits held in acc (< 32 between emits)
-  uint32_t widx;   // chunk-relative index of the word being filled
-  uint32_t wbase;  // first word of the LDS window
-  uint32_t *win;
-  uint32_t cap;    // window size in words
+  int nacc;          // bits held in acc (< 32 between emits)
+  uint32_t widx;     // chunk-relative index of the word being filled
+  uint32_t fw, lw;   // the block's first and last word
+  uint32_t *slot;
+  uint32_t head, tail;
   __device__ __forceinline__ void put(uint32_t w) {
-    const uint32_t i = widx - wbase;
-    if (i < cap) atomicOr(&win[i], w);
+    if (widx == fw)
+      head = w;
+    else if (widx == lw)
+      tail = w;
+    else
+      slot[widx] = w;
     widx++;
   }
   __device__ __forceinline__ void emit(uint32_t v, int n) {
@@ -319,7 +334,6 @@ __device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s
 // Persistent grid: wave w encodes chunks [w*T, (w+1)*T) in (frame, chunk) order and
 // prefetches the next chunk's pixel rows into registers while encoding the current one.
 constexpr int kWavesPerWg = 4;
-constexpr int kWaveWinWords = 256;  // per-wave bit-pack window (1 KiB); heavier chunks loop
 
 __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g, int frame, int b) {
   const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
@@ -394,7 +408,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) int s_m2[72];       // pass-2 dot rows + per-row constant
-  __shared__ uint32_t s_win_all[kWavesPerWg][kWaveWinWords];
+  __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -405,11 +419,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_zz[tid] = kZigzag[tid];
     s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     s_m2[tid] = kPass2Dot[tid];
+    s_scat[tid] = kScreenScatter[tid];
   }
   if (tid < 8) s_m2[64 + tid] = kPass2Add[tid];
-  uint32_t *s_win = s_win_all[wave];
   uint32_t *s_pk = s_pk_all[wave];
-  for (int i = lane; i < kWaveWinWords; i += 64) s_win[i] = 0;
   __syncthreads();  // tables visible; the only workgroup barrier
 
   const int nwaves = gridDim.x * kWavesPerWg;
@@ -463,6 +476,13 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // butterfly's differences cancel and its sums remove with one -2M.
     const float rA = tab ? 0x1.237p+0f : 0x1.2a14p+0f;        // 2387456 / 2^21, 2441856 / 2^21
     const float rB = tab ? -0x1.1b821p+4f : -0x1.29fbe8p+4f;  // -17.719253..., -18.624000...
+#if MJG_ABLATE == 3
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) s_pk[(r * 4 + j) * 64 + lane] = (uint32_t)(raw[r] >> (16 * (j & 1)));
+    if (false)
+#endif
 #pragma unroll
     for (int r = 0; r < 8; r++) {
       const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
@@ -538,7 +558,12 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // (exact_coef).  Rows 0 and 4 (sums only) are exact, which gives the DC exactly:
     // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
     int dc = 0;
-    uint32_t mlo = 0, mhi = 0;
+    uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
+#if MJG_ABLATE >= 2 && MJG_ABLATE <= 3
+    ca = s_pk[lane] & 0x10101010u;
+    cb = s_pk[64 + lane] & 0x1010u;
+    if (false)
+#endif
     if (cur_active) {
 #pragma unroll
       for (int jp = 0; jp < 4; jp++) {
@@ -573,15 +598,16 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
           const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
 #pragma unroll
           for (int r = 0; r < 8; r++) {
-            const int k = kZigzagInv[r * 8 + col];
-            if (k == 0) {
+            if (col == 0 && r == 0) {
               dc = (int)(__float_as_uint(__builtin_fmaf(sv[0], 1.0f / 1024, 0x1.1p-7f) + kM) - 0x4B400000u);
             } else {
+              // sign of B^2 - s^2 shifted into the candidate word in computation order
+              // (v_alignbit: (m << 1) | (neg >> 31)); zigzag order is restored below
               const uint32_t neg = __float_as_uint(__builtin_fmaf(-sv[r], sv[r], thr[r]));
-              if (k < 32)
-                mlo |= (neg >> (31 - k)) & (1u << k);
+              if (col < 4)
+                ca = __builtin_amdgcn_alignbit(ca, neg, 31);
               else
-                mhi |= (neg >> (63 - k)) & (1u << (k - 32));
+                cb = __builtin_amdgcn_alignbit(cb, neg, 31);
             }
           }
         }
@@ -596,7 +622,18 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
         }
       }
     }
-    const uint64_t mask = ((uint64_t)mhi << 32) | mlo;
+    // candidate bits -> zigzag-ordered mask (a handful of candidates per block)
+    uint64_t mask = 0;
+    while (ca) {
+      const int pos = __builtin_ctz(ca);
+      ca &= ca - 1;
+      mask |= 1ull << s_scat[pos];
+    }
+    while (cb) {
+      const int pos = __builtin_ctz(cb);
+      cb &= cb - 1;
+      mask |= 1ull << s_scat[32 + pos];
+    }
 
     // DC predictor (FFmpeg last_dc, 128 at every frame start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.
@@ -608,7 +645,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     carry = dc;
 
     RegSink q;
-#if MJG_ABLATE == 0
+#if MJG_ABLATE == 0 || MJG_ABLATE == 4
     if (cur_active) {
       emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, q);
       q.finish();
@@ -622,42 +659,58 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const uint32_t incl = wave_incl_scan(q.bits, lane);
     const uint32_t off = incl - q.bits;
     const uint32_t total = __shfl(incl, 63, 64);
-    const uint32_t nwords = (total + 31) >> 5;
     uint32_t *slot = scratch + (size_t)t * kSlotWords;
 
-    for (uint32_t wbase = 0; wbase < nwords; wbase += kWaveWinWords) {
-      const uint32_t first_w = off >> 5, last_w = (off + q.bits - 1) >> 5;
-      if (cur_active && last_w >= wbase && first_w < wbase + kWaveWinWords) {
-        if (q.bits <= 128) {
-          // shift the queued words to the block's offset: up to 5 destination words
-          const uint32_t s = off & 31;
-          const uint32_t w[4] = {q.w0, q.w1, q.w2, q.w3};
+    // Pack into the chunk slot without LDS atomics.  Lane L's bits occupy words fw..lw.
+    // Words strictly inside are L's alone; word fw may be shared with earlier lanes and
+    // word lw with later ones.  Every word has one writer: the lane whose bits cover its
+    // first bit ("opener"), which ORs in the heads of the lanes that start inside the
+    // word, G = segmented suffix-OR of heads over lanes with equal fw.
+    const bool has = cur_active && q.bits != 0;
+    const uint32_t sft = off & 31, fw = off >> 5;
+    const uint32_t lw = has ? (off + q.bits - 1) >> 5 : fw;
+    uint32_t head = 0, tail = 0;
+    if (has && MJG_ABLATE != 4) {
+      if (q.bits <= 128) {
+        const uint32_t w[5] = {q.w0, q.w1, q.w2, q.w3, 0u};
+        head = w[0] >> sft;
+        const uint32_t nmid = lw - fw;  // 0..4
 #pragma unroll
-          for (int i = 0; i < 5; i++) {
-            if ((uint32_t)i <= last_w - first_w) {
-              const uint32_t hi = i < 4 ? (s ? w[i] >> s : w[i]) : 0u;
-              const uint32_t lo = (i > 0 && s) ? w[i - 1] << (32 - s) : 0u;
-              const uint32_t idx = first_w + i - wbase;
-              if (idx < (uint32_t)kWaveWinWords) atomicOr(&s_win[idx], hi | lo);
-            }
+        for (int i = 1; i < 5; i++) {
+          if ((uint32_t)i <= nmid) {
+            const uint32_t v = sft ? (w[i] >> sft) | (w[i - 1] << (32 - sft)) : w[i];
+            if ((uint32_t)i < nmid)
+              slot[fw + i] = v;
+            else
+              tail = v;
           }
-        } else {  // long block: re-emit straight into the window at its offset
-          BitSink sink;
-          sink.acc = 0;
-          sink.nacc = (int)(off & 31);
-          sink.widx = first_w;
-          sink.wbase = wbase;
-          sink.win = s_win;
-          sink.cap = kWaveWinWords;
-          emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, sink);
-          sink.finish();
         }
+      } else {  // long block: re-emit, interior words straight to the slot
+        SlotSink sink;
+        sink.acc = 0;
+        sink.nacc = (int)sft;
+        sink.widx = fw;
+        sink.fw = fw;
+        sink.lw = lw;
+        sink.slot = slot;
+        sink.head = 0;
+        sink.tail = 0;
+        emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, sink);
+        sink.finish();
+        head = sink.head;
+        tail = sink.tail;
       }
-      const uint32_t n = min((uint32_t)kWaveWinWords, nwords - wbase);
-      for (uint32_t i = lane; i < n; i += 64) {
-        slot[wbase + i] = s_win[i];
-        s_win[i] = 0;  // ready for the next window / chunk
-      }
+    }
+    uint32_t grp = head;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_down(grp, d, 64), f = __shfl_down(fw, d, 64);
+      if (lane + d < 64 && f == fw) grp |= v;
+    }
+    const uint32_t gnext = __shfl_down(grp, 1, 64), fnext = __shfl_down(fw, 1, 64);
+    if (has && MJG_ABLATE != 4) {
+      if (lw > fw) slot[lw] = tail | ((lane < 63 && fnext == lw) ? gnext : 0u);
+      if (sft == 0) slot[fw] = grp;  // word-aligned start: this lane opens word fw
     }
     if (lane == 0) chunk_bits[t] = total;
     if (tn < 0) break;

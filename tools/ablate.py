@@ -15,7 +15,7 @@ CSRC = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
 def build(n, extra=()):
     out = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_ablate{n}.so")
     if "--build" in sys.argv or not os.path.exists(out):
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
                f"-DMJG_ABLATE={n}", "-I", os.path.join(ROOT, "include"), "-o", out,
                os.path.join(CSRC, "api.hip"), os.path.join(CSRC, "sws_filter.cpp"), *extra]
         subprocess.run(cmd, check=True, cwd=CSRC)

@@ -23,7 +23,7 @@ def parse():
 
 def build(name, src, flags):
     so = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
            *flags, "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(src, "api.hip"),
            os.path.join(CSRC, "sws_filter.cpp")]
     subprocess.run(cmd, check=True, cwd=src)
