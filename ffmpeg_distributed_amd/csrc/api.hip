@@ -146,7 +146,7 @@ struct mjg_ctx {
   uint8_t *d_hdr = nullptr;
   uint8_t *d_stage = nullptr, *d_scaled = nullptr;
   uint32_t *d_scratch = nullptr;
-  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_chunk_ff = nullptr, *d_ff_off = nullptr;
+  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
   uint32_t *d_frame_bits = nullptr, *d_status = nullptr, *d_work = nullptr;
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
   uint8_t *d_out = nullptr;
@@ -173,7 +173,7 @@ void free_ctx(mjg_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
-                  c->d_chunk_off, c->d_chunk_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
+                  c->d_chunk_off, c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
                   c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->ps[0].hc,
                   c->ps[0].vc, c->ps[0].hp, c->ps[0].vp, c->ps[1].hc, c->ps[1].vc, c->ps[1].hp,
                   c->ps[1].vp};
@@ -311,7 +311,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
       (rc = dmalloc(&c->d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
-      (rc = dmalloc(&c->d_chunk_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
+      (rc = dmalloc(&c->d_group_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
       (rc = dmalloc(&c->d_frame_bits, B)) || (rc = dmalloc(&c->d_status, 4)) ||
       (rc = dmalloc(&c->d_work, 1)) ||
       (rc = dmalloc(&c->d_frame_size, B)) || (rc = dmalloc(&c->d_frame_offsets, B + 1)))
@@ -485,13 +485,13 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_COUNT_FF, 0);
   const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
   k_count_ff<<<(gpf * n + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits, c->d_chunk_off,
-                                                       c->d_frame_bits, c->d_chunk_ff, g.nchunks,
+                                                       c->d_frame_bits, c->d_group_ff, g.nchunks,
                                                        gpf, gpf * n);
   tmark(c, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_FF, 0);
-  k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_chunk_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
-                                       g.nchunks, (int)c->hdr.size());
+  k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
+                                       gpf, (int)c->hdr.size());
   tmark(c, MJG_K_SCAN_FF, 1);
   HIP_TRY(hipGetLastError());
   int rc = launch_write(c, n);

@@ -813,45 +813,82 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
-// Wave per run of kChunksPerWave chunks of one frame (4 waves per workgroup), lane = word:
-// realign each chunk's words to its frame offset and count the 0xFF bytes among the bytes
-// it owns (a byte belongs to the chunk holding its first bit).  A chunk is ~27 words at
-// 4K q5, so one chunk per wave left the launch dominated by wave start-up.
+// Realign/stuff kernels work on *groups* of kChunksPerWave consecutive chunks of a frame,
+// one wave per group, lanes = the group's words flattened across its chunks.  A word
+// belongs to the chunk holding its first bit, so chunk c owns words
+// [ceil(O_c / 32), ceil(O_{c+1} / 32)) and a group owns one contiguous word range.
 constexpr int kChunksPerWave = 8;
+
+struct GroupWords {
+  int f, c0, n;          // frame, first chunk, chunks in the group
+  uint32_t T, total_bytes;
+  uint32_t k0, k1;       // owned word range
+  uint32_t o_lane;       // lane j < n: O_{c0+j}; lane n: end offset of the group
+  const uint32_t *chunk_off, *chunk_bits;  // the group's first chunk
+};
+
+__device__ __forceinline__ GroupWords group_words(const uint32_t *chunk_bits, const uint32_t *chunk_off,
+                                                  const uint32_t *frame_bits, int nchunks,
+                                                  int ngroups_per_frame, int gi, int lane) {
+  GroupWords g;
+  g.f = gi / ngroups_per_frame;
+  g.c0 = (gi - g.f * ngroups_per_frame) * kChunksPerWave;
+  g.n = min(kChunksPerWave, nchunks - g.c0);
+  g.T = frame_bits[g.f];
+  g.total_bytes = (g.T + 7) >> 3;
+  const size_t i0 = (size_t)g.f * nchunks + g.c0;
+  g.chunk_off = chunk_off + i0;
+  g.chunk_bits = chunk_bits + i0;
+  g.o_lane = lane < g.n ? chunk_off[i0 + lane] : 0u;
+  const uint32_t last = __shfl(g.o_lane, g.n - 1, 64) + chunk_bits[i0 + g.n - 1];
+  if (lane == g.n) g.o_lane = last;
+  g.k0 = (__shfl(g.o_lane, 0, 64) + 31) >> 5;
+  g.k1 = (last + 31) >> 5;
+  return g;
+}
+
+// Owner chunk (relative to the group) of word k, its offset O and length L.
+__device__ __forceinline__ int word_owner(const GroupWords &g, uint32_t k, uint32_t &O, uint32_t &L) {
+  int c = 0;
+#pragma unroll
+  for (int j = 1; j < kChunksPerWave; j++) {
+    const uint32_t oj = __builtin_amdgcn_readlane(g.o_lane, j);
+    c += (j < g.n && k >= ((oj + 31) >> 5)) ? 1 : 0;
+  }
+  O = g.chunk_off[c];
+  L = g.chunk_bits[c];
+  return c;
+}
 
 __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
                                                   const uint32_t *__restrict__ chunk_bits,
                                                   const uint32_t *__restrict__ chunk_off,
                                                   const uint32_t *__restrict__ frame_bits,
-                                                  uint32_t *__restrict__ chunk_ff, int nchunks,
+                                                  uint32_t *__restrict__ group_ff, int nchunks,
                                                   int ngroups_per_frame, int ngroups) {
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (gi >= ngroups) return;
-  const int f = gi / ngroups_per_frame;
-  const int c0 = (gi - f * ngroups_per_frame) * kChunksPerWave;
-  const int c1 = min(c0 + kChunksPerWave, nchunks);
-  const uint32_t T = frame_bits[f];
-  const uint32_t total_bytes = (T + 7) >> 3;
-  for (int c = c0; c < c1; c++) {
-    const int i = f * nchunks + c;
-    const uint32_t O = chunk_off[i], L = chunk_bits[i];
-    const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-    int cnt = 0;
-    for (uint32_t k = k0 + lane; k < k1; k += 64)
-      cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k), 4 * k, total_bytes);
-    cnt = wave_sum(cnt);
-    if (lane == 0) chunk_ff[i] = (uint32_t)cnt;
+  const GroupWords g = group_words(chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
+  int cnt = 0;
+  for (uint32_t k = g.k0 + lane; k < g.k1; k += 64) {
+    uint32_t O, L;
+    const int c = word_owner(g, k, O, L);
+    cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, g.f, g.c0 + c, O, L, g.T, k), 4 * k,
+                      g.total_bytes);
   }
+  cnt = wave_sum(cnt);
+  if (lane == 0) group_ff[gi] = (uint32_t)cnt;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ chunk_ff,
+// Per frame: exclusive scan of the chunk groups' 0xFF counts -> stuffed frame size.
+__global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ group_ff,
                                                   uint32_t *__restrict__ ff_off,
                                                   const uint32_t *__restrict__ frame_bits,
-                                                  uint64_t *__restrict__ frame_size, int nchunks,
+                                                  uint64_t *__restrict__ frame_size, int ngroups_per_frame,
                                                   int hdr_len) {
   const int f = blockIdx.x;
-  const uint32_t t = block_excl_scan(chunk_ff + (size_t)f * nchunks, ff_off + (size_t)f * nchunks,
-                                     nchunks);
+  const size_t g0 = (size_t)f * ngroups_per_frame;
+  const uint32_t t = block_excl_scan(group_ff + g0, ff_off + g0, ngroups_per_frame);
   if (threadIdx.x == 0) frame_size[f] = (uint64_t)hdr_len + ((frame_bits[f] + 7) >> 3) + t + 2;
 }
 
@@ -884,9 +921,9 @@ __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ f
   }
 }
 
-// Wave per run of kChunksPerWave chunks, lane = word: each chunk's owned bytes with a
-// 0x00 after every 0xFF (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs
-// before it in the frame (chunk prefix from k_scan_ff, in-chunk prefix by a wave scan).
+// Wave per chunk group, lanes = words: the group's owned bytes with a 0x00 after every
+// 0xFF (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs before it in the
+// frame (group prefix from k_scan_ff, in-group prefix by a wave scan).
 __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
     const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
@@ -895,40 +932,33 @@ __global__ __launch_bounds__(256) void k_write(
     int ngroups, uint8_t *__restrict__ out, uint64_t out_cap) {
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (gi >= ngroups) return;
-  const int f = gi / ngroups_per_frame;
-  const int c0 = (gi - f * ngroups_per_frame) * kChunksPerWave;
-  const int c1 = min(c0 + kChunksPerWave, nchunks);
-  const uint64_t foff = frame_offsets[f];
-  if (foff + frame_size[f] > out_cap) return;  // k_frame_hdr flagged the overflow
-  const uint32_t T = frame_bits[f];
-  const uint32_t total_bytes = (T + 7) >> 3;
-  for (int c = c0; c < c1; c++) {
-    const int i = f * nchunks + c;
-    const uint32_t O = chunk_off[i], L = chunk_bits[i];
-    const uint32_t k0 = (O + 31) >> 5, k1 = (O + L + 31) >> 5;
-    uint8_t *base = out + foff + hdr_len + 4 * (size_t)k0 + ff_off[i];
-    uint32_t carry = 0;
-    for (uint32_t kb = k0; kb < k1; kb += 64) {
-      const uint32_t k = kb + lane;
-      uint32_t v = 0, cnt = 0;
-      if (k < k1) {
-        v = aligned_word(scratch, chunk_bits, nchunks, f, c, O, L, T, k);
-        cnt = (uint32_t)ff_in_word(v, 4 * k, total_bytes);
-      }
-      const uint32_t incl = wave_incl_scan(cnt, lane);
-      if (k < k1) {
-        uint8_t *p = base + 4 * (k - k0) + carry + incl - cnt;
+  const GroupWords g = group_words(chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
+  const uint64_t foff = frame_offsets[g.f];
+  if (foff + frame_size[g.f] > out_cap) return;  // k_frame_hdr flagged the overflow
+  uint8_t *base = out + foff + hdr_len + 4 * (size_t)g.k0 + ff_off[gi];
+  uint32_t carry = 0;
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64) {
+    const uint32_t k = kb + lane;
+    uint32_t v = 0, cnt = 0;
+    if (k < g.k1) {
+      uint32_t O, L;
+      const int c = word_owner(g, k, O, L);
+      v = aligned_word(scratch, chunk_bits, nchunks, g.f, g.c0 + c, O, L, g.T, k);
+      cnt = (uint32_t)ff_in_word(v, 4 * k, g.total_bytes);
+    }
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    if (k < g.k1) {
+      uint8_t *p = base + 4 * (k - g.k0) + carry + incl - cnt;
 #pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-          if (4 * k + bb < total_bytes) {
-            const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
-            *p++ = byte;
-            if (byte == 0xff) *p++ = 0;
-          }
+      for (int bb = 0; bb < 4; bb++) {
+        if (4 * k + bb < g.total_bytes) {
+          const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
+          *p++ = byte;
+          if (byte == 0xff) *p++ = 0;
         }
       }
-      carry += __shfl(incl, 63, 64);
     }
+    carry += __shfl(incl, 63, 64);
   }
 }
 
