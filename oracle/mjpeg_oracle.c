@@ -5,7 +5,7 @@
  * external `ffmpeg` worker (ffmpeg_distributed.py:131-141 spawns
  * `ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:`), restricted to the
  * north-star profile  [-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int
- * -huffman default -bitexact  on yuv420p / yuvj420p frames.
+ * -huffman default|optimal -bitexact  on yuv420p / yuvj420p frames.
  *
  * The arithmetic lives in third-party FFmpeg (libavcodec mjpeg encoder, libswscale),
  * which is NOT vendored under /root/reference, not pinned by it (no requirements
@@ -298,13 +298,14 @@ typedef struct {
     uint8_t ac_size[2][256]; uint16_t ac_code[2][256];
 } or_huff;
 
-static void or_huff_init(or_huff *h)
+static void or_huff_init_tables(or_huff *h, const uint8_t *const bits[4], const uint8_t *const vals[4])
 {
-    or_build_huff(h->dc_size[0], h->dc_code[0], or_bits_dc_lum, or_val_dc);
-    or_build_huff(h->dc_size[1], h->dc_code[1], or_bits_dc_chr, or_val_dc);
-    or_build_huff(h->ac_size[0], h->ac_code[0], or_bits_ac_lum, or_val_ac_lum);
-    or_build_huff(h->ac_size[1], h->ac_code[1], or_bits_ac_chr, or_val_ac_chr);
+    or_build_huff(h->dc_size[0], h->dc_code[0], bits[0], vals[0]);
+    or_build_huff(h->dc_size[1], h->dc_code[1], bits[1], vals[1]);
+    or_build_huff(h->ac_size[0], h->ac_code[0], bits[2], vals[2]);
+    or_build_huff(h->ac_size[1], h->ac_code[1], bits[3], vals[3]);
 }
+
 
 static int or_log2_16(int v) { int n = 0; while (v >> (n + 1)) n++; return n; }
 
@@ -349,6 +350,28 @@ static void or_encode_block(or_pb *pb, const or_huff *h, const int16_t *block, i
         pb_put(pb, h->ac_size[tab][0], h->ac_code[tab][0]);
 }
 
+/* mjpegenc.c record_block / ff_mjpeg_encode_coef / ff_mjpeg_encode_code (-huffman
+ * optimal): the same symbols encode_block emits, counted per table (0 DC lum, 1 DC chr,
+ * 2 AC lum, 3 AC chr) as mjpeg_build_optimal_huffman does over the picture's buffer. */
+static void or_count_block(uint32_t counts[4][256], const int16_t *block, int n, int last_index,
+                           int *last_dc)
+{
+    int component = (n <= 3) ? 0 : (n & 1) + 1;
+    int tab = (n <= 3) ? 0 : 1;
+    int dc = block[0], val = dc - last_dc[component];
+    last_dc[component] = dc;
+    counts[tab][val == 0 ? 0 : or_log2_16(val < 0 ? -val : val) + 1]++;
+    int run = 0;
+    for (int i = 1; i <= last_index; i++) {
+        int v = block[or_zigzag[i]];
+        if (v == 0) { run++; continue; }
+        while (run >= 16) { counts[2 + tab][0xf0]++; run -= 16; }
+        counts[2 + tab][(run << 4) | (or_log2_16(v < 0 ? -v : v) + 1)]++;
+        run = 0;
+    }
+    if (last_index < 63 || run != 0) counts[2 + tab][0]++;
+}
+
 /* ---------------------------------------------------------------- header */
 /* mjpegenc_common.c ff_mjpeg_encode_picture_header + jpeg_put_comments +
  * jpeg_table_header, for AV_CODEC_ID_MJPEG, 4:2:0, -bitexact (no COM Lavc),
@@ -366,8 +389,9 @@ static int put_huffman_table(or_pb *pb, int cls, int id, const uint8_t *bits, co
     return n + 17;
 }
 
-size_t or_header(int width, int height, int qscale, int sar_num, int sar_den, int com_itu601,
-                 int dri_interval, uint8_t *out, size_t cap)
+static size_t or_header_tables(int width, int height, int qscale, int sar_num, int sar_den,
+                               int com_itu601, int dri_interval, const uint8_t *const bits[4],
+                               const uint8_t *const vals[4], uint8_t *out, size_t cap)
 {
     or_pb pb = { out, cap, 0, 0 };
     uint8_t mprime[64]; int32_t qmat[64];
@@ -395,10 +419,11 @@ size_t or_header(int width, int height, int qscale, int sar_num, int sar_den, in
     size_t len_pos = pb.nbits >> 3;
     put16(&pb, 0);
     int size = 2;
-    size += put_huffman_table(&pb, 0, 0, or_bits_dc_lum, or_val_dc);
-    size += put_huffman_table(&pb, 0, 1, or_bits_dc_chr, or_val_dc);
-    size += put_huffman_table(&pb, 1, 0, or_bits_ac_lum, or_val_ac_lum);
-    size += put_huffman_table(&pb, 1, 1, or_bits_ac_chr, or_val_ac_chr);
+    /* jpeg_table_header: one DHT, order DC0, DC1, AC0, AC1 (default or optimal tables) */
+    size += put_huffman_table(&pb, 0, 0, bits[0], vals[0]);
+    size += put_huffman_table(&pb, 0, 1, bits[1], vals[1]);
+    size += put_huffman_table(&pb, 1, 0, bits[2], vals[2]);
+    size += put_huffman_table(&pb, 1, 1, bits[3], vals[3]);
     if (len_pos + 1 < cap) { out[len_pos] = (uint8_t)(size >> 8); out[len_pos + 1] = (uint8_t)size; }
     put16(&pb, 0xFFC0); put16(&pb, 17); put8(&pb, 8);   /* SOF0 */
     put16(&pb, height); put16(&pb, width); put8(&pb, 3);
@@ -412,6 +437,196 @@ size_t or_header(int width, int height, int qscale, int sar_num, int sar_den, in
     put8(&pb, 0); put8(&pb, 63); put8(&pb, 0);
     if (pb.overflow) return 0;
     return pb.nbits >> 3;
+}
+
+static const uint8_t *const or_default_bits[4] = { or_bits_dc_lum, or_bits_dc_chr, or_bits_ac_lum, or_bits_ac_chr };
+static const uint8_t *const or_default_vals[4] = { or_val_dc, or_val_dc, or_val_ac_lum, or_val_ac_chr };
+
+size_t or_header(int width, int height, int qscale, int sar_num, int sar_den, int com_itu601,
+                 int dri_interval, uint8_t *out, size_t cap)
+{
+    return or_header_tables(width, height, qscale, sar_num, sar_den, com_itu601, dri_interval,
+                            or_default_bits, or_default_vals, out, cap);
+}
+
+/* ------------------------------------------------- -huffman optimal tables */
+/* libavutil/qsort.h AV_QSORT (the in-place median-of-3 quicksort with an explicit stack
+ * and the "already sorted" early exit), restated over elements of `size` bytes.  The
+ * tie order it leaves matters: mjpegenc_huffman.c sorts symbol counts with it before
+ * package-merge, and equal counts can end up with different code lengths. */
+typedef int (*or_cmp_fn)(const void *, const void *);
+static void or_memswap(void *a, void *b, size_t size)
+{
+    uint8_t t[16], *x = (uint8_t *)a, *y = (uint8_t *)b;
+    if (a == b) return;
+    memcpy(t, x, size); memcpy(x, y, size); memcpy(y, t, size);
+}
+static void or_av_qsort(void *base, int num, size_t size, or_cmp_fn cmp)
+{
+#define E(i) ((uint8_t *)base + (size_t)(i) * size)
+    int stack[64][2];
+    int sp = 1;
+    stack[0][0] = 0;
+    stack[0][1] = num - 1;
+    while (sp) {
+        int start = stack[--sp][0];
+        int end = stack[sp][1];
+        while (start < end) {
+            if (start < end - 1) {
+                int checksort = 0;
+                int right = end - 2;
+                int left = start + 1;
+                int mid = start + ((end - start) >> 1);
+                if (cmp(E(start), E(end)) > 0) {
+                    if (cmp(E(end), E(mid)) > 0) or_memswap(E(start), E(mid), size);
+                    else                         or_memswap(E(start), E(end), size);
+                } else {
+                    if (cmp(E(start), E(mid)) > 0) or_memswap(E(start), E(mid), size);
+                    else checksort = 1;
+                }
+                if (cmp(E(mid), E(end)) > 0) {
+                    or_memswap(E(mid), E(end), size);
+                    checksort = 0;
+                }
+                if (start == end - 2) break;
+                or_memswap(E(end - 1), E(mid), size);
+                while (left <= right) {
+                    while (left <= right && cmp(E(left), E(end - 1)) < 0) left++;
+                    while (left <= right && cmp(E(right), E(end - 1)) > 0) right--;
+                    if (left <= right) {
+                        or_memswap(E(left), E(right), size);
+                        left++;
+                        right--;
+                    }
+                }
+                or_memswap(E(end - 1), E(left), size);
+                if (checksort && (mid == left - 1 || mid == left)) {
+                    mid = start;
+                    while (mid < end && cmp(E(mid), E(mid + 1)) <= 0) mid++;
+                    if (mid == end) break;
+                }
+                if (end - left < left - start) {
+                    stack[sp][0] = start;
+                    stack[sp++][1] = right;
+                    start = left + 1;
+                } else {
+                    stack[sp][0] = left + 1;
+                    stack[sp++][1] = end;
+                    end = right;
+                }
+            } else {
+                if (cmp(E(start), E(end)) > 0) or_memswap(E(start), E(end), size);
+                break;
+            }
+        }
+    }
+#undef E
+}
+
+/* mjpegenc_huffman.h PTable / HuffTable */
+typedef struct { int value; int prob; } or_ptable;
+typedef struct { int code; int length; } or_hufftable;
+
+static int or_cmp_prob(const void *a, const void *b)
+{
+    return ((const or_ptable *)a)->prob - ((const or_ptable *)b)->prob;
+}
+static int or_cmp_length(const void *a, const void *b)
+{
+    const or_hufftable *x = (const or_hufftable *)a, *y = (const or_hufftable *)b;
+    if (x->length == y->length) return x->code - y->code;
+    return x->length - y->length;
+}
+
+/* mjpegenc_huffman.c ff_mjpegenc_huffman_compute_bits: package-merge limited to
+ * max_length bits over prob_table (sorted here with AV_QSORT). */
+typedef struct {
+    int nitems;
+    int item_idx[515];
+    int probability[514];
+    int items[257 * 16];
+} or_pm_list;
+
+static void or_huffman_compute_bits(or_ptable *prob_table, or_hufftable *distincts, int size,
+                                    int max_length, int *ndistinct)
+{
+    static or_pm_list list_a, list_b;  /* large; the oracle is single-threaded per process */
+    or_pm_list *to = &list_a, *from = &list_b, *temp;
+    int times, i = 0, j, k;
+    int nbits[257] = { 0 };
+    int min;
+
+    to->nitems = 0;
+    from->nitems = 0;
+    to->item_idx[0] = 0;
+    from->item_idx[0] = 0;
+    or_av_qsort(prob_table, size, sizeof(or_ptable), or_cmp_prob);
+
+    for (times = 0; times <= max_length; times++) {
+        to->nitems = 0;
+        to->item_idx[0] = 0;
+        j = 0;
+        k = 0;
+        if (times < max_length) i = 0;
+        while (i < size || j + 1 < from->nitems) {
+            to->nitems++;
+            to->item_idx[to->nitems] = to->item_idx[to->nitems - 1];
+            if (i < size &&
+                (j + 1 >= from->nitems ||
+                 prob_table[i].prob < from->probability[j] + from->probability[j + 1])) {
+                to->items[to->item_idx[to->nitems]++] = prob_table[i].value;
+                to->probability[to->nitems - 1] = prob_table[i].prob;
+                i++;
+            } else {
+                for (k = from->item_idx[j]; k < from->item_idx[j + 2]; k++)
+                    to->items[to->item_idx[to->nitems]++] = from->items[k];
+                to->probability[to->nitems - 1] = from->probability[j] + from->probability[j + 1];
+                j += 2;
+            }
+        }
+        temp = to;
+        to = from;
+        from = temp;
+    }
+
+    min = (size - 1 < from->nitems) ? size - 1 : from->nitems;
+    for (i = 0; i < from->item_idx[min]; i++) nbits[from->items[i]]++;
+    /* the 256 entry only prevents an all-ones code; it is not returned */
+    j = 0;
+    for (i = 0; i < 256; i++) {
+        if (nbits[i] > 0) {
+            distincts[j].code = i;
+            distincts[j].length = nbits[i];
+            j++;
+        }
+    }
+    *ndistinct = j;
+}
+
+/* mjpegenc_huffman.c ff_mjpeg_encode_huffman_close: BITS/HUFFVAL of the optimal code for
+ * one table's symbol counts.  Returns the number of values. */
+int or_huff_optimal(const uint32_t counts[256], uint8_t bits[17], uint8_t vals[256])
+{
+    or_ptable val_counts[257];
+    or_hufftable distincts[256];
+    int nval = 0, nd = 0;
+    for (int i = 0; i < 256; i++) {
+        if (counts[i]) {
+            val_counts[nval].value = i;
+            val_counts[nval].prob = (int)counts[i];
+            nval++;
+        }
+    }
+    val_counts[nval].value = 256;
+    val_counts[nval].prob = 0;
+    or_huffman_compute_bits(val_counts, distincts, nval + 1, 16, &nd);
+    or_av_qsort(distincts, nval, sizeof(or_hufftable), or_cmp_length);
+    memset(bits, 0, 17);
+    for (int i = 0; i < nval; i++) {
+        vals[i] = (uint8_t)distincts[i].code;
+        bits[distincts[i].length]++;
+    }
+    return nval;
 }
 
 /* ------------------------------------------------------- block gathering */
@@ -458,12 +673,10 @@ int or_frame_coeffs(const uint8_t *y, int ys, const uint8_t *u, int us, const ui
 /* mjpegenc_common.c ff_mjpeg_escape_FF + ff_mjpeg_encode_stuffing: pad the scan
  * with 1-bits to a byte boundary, insert 0x00 after every 0xFF of the scan data;
  * then EOI (ff_mjpeg_encode_picture_trailer). */
-size_t or_encode_planes(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
-                        int w, int h, int qscale, int sar_num, int sar_den, int com_itu601,
-                        uint8_t *out, size_t cap)
+size_t or_encode_planes_ex(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                           int w, int h, int qscale, int sar_num, int sar_den, int com_itu601,
+                           int huff_optimal, uint8_t *out, size_t cap)
 {
-    size_t hdr = or_header(w, h, qscale, sar_num, sar_den, com_itu601, 0, out, cap);
-    if (!hdr) return 0;
     int mbw = (w + 15) / 16, mbh = (h + 15) / 16;
     size_t nblocks = (size_t)mbw * mbh * 6;
     int16_t *coef = (int16_t *)malloc(nblocks * 64 * sizeof(int16_t));
@@ -471,7 +684,28 @@ size_t or_encode_planes(const uint8_t *y, int ys, const uint8_t *u, int us, cons
     if (!coef || !last) { free(coef); free(last); return 0; }
     or_frame_coeffs(y, ys, u, us, v, vs, w, h, qscale, coef, last);
 
-    or_huff hf; or_huff_init(&hf);
+    const uint8_t *bits[4], *vals[4];
+    uint8_t obits[4][17], ovals[4][256];
+    for (int t = 0; t < 4; t++) { bits[t] = or_default_bits[t]; vals[t] = or_default_vals[t]; }
+    if (huff_optimal) {
+        /* mjpegenc.c ff_mjpeg_encode_stuffing -> mjpeg_build_optimal_huffman: the
+         * picture's symbols are buffered, counted, and the tables built before the
+         * header and the scan are written. */
+        static uint32_t counts[4][256];
+        int last_dc[3] = { 128, 128, 128 };
+        memset(counts, 0, sizeof counts);
+        for (size_t b = 0; b < nblocks; b++)
+            or_count_block(counts, coef + b * 64, (int)(b % 6), last[b], last_dc);
+        for (int t = 0; t < 4; t++) {
+            or_huff_optimal(counts[t], obits[t], ovals[t]);
+            bits[t] = obits[t];
+            vals[t] = ovals[t];
+        }
+    }
+    size_t hdr = or_header_tables(w, h, qscale, sar_num, sar_den, com_itu601, 0, bits, vals, out, cap);
+    if (!hdr) { free(coef); free(last); return 0; }
+
+    or_huff hf; or_huff_init_tables(&hf, bits, vals);
     or_pb pb = { out + hdr, cap - hdr, 0, 0 };
     int last_dc[3] = { 128, 128, 128 };
     for (size_t b = 0; b < nblocks; b++)
@@ -495,6 +729,14 @@ size_t or_encode_planes(const uint8_t *y, int ys, const uint8_t *u, int us, cons
     size_t total = hdr + size + nff;
     out[total] = 0xFF; out[total + 1] = 0xD9;         /* EOI */
     return total + 2;
+}
+
+size_t or_encode_planes(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                        int w, int h, int qscale, int sar_num, int sar_den, int com_itu601,
+                        uint8_t *out, size_t cap)
+{
+    return or_encode_planes_ex(y, ys, u, us, v, vs, w, h, qscale, sar_num, sar_den, com_itu601, 0,
+                               out, cap);
 }
 
 /* ================================================================ swscale */
@@ -707,13 +949,15 @@ int or_local_pos(int sub, int pos)
 /* Full worker path for one yuv420p/yuvj420p frame: optional bicubic resize and
  * the auto-inserted tv->pc conversion (swscale context yuv420p -> yuvj420p), then
  * the mjpeg encode.  in_full_range: 1 for yuvj420p input (no conversion). */
-size_t or_encode_frame(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
-                       int sw, int sh, int dw, int dh, int in_full_range, int qscale,
-                       int sar_num, int sar_den, int bitexact_sws, uint8_t *out, size_t cap)
+size_t or_encode_frame_ex(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                          int sw, int sh, int dw, int dh, int in_full_range, int qscale,
+                          int sar_num, int sar_den, int bitexact_sws, int huff_optimal,
+                          uint8_t *out, size_t cap)
 {
     int need_sws = (sw != dw || sh != dh || !in_full_range);
     if (!need_sws)
-        return or_encode_planes(y, ys, u, us, v, vs, sw, sh, qscale, sar_num, sar_den, 0, out, cap);
+        return or_encode_planes_ex(y, ys, u, us, v, vs, sw, sh, qscale, sar_num, sar_den, 0, huff_optimal,
+                                   out, cap);
     int dcw = (dw + 1) >> 1, dch = (dh + 1) >> 1, scw = (sw + 1) >> 1, sch = (sh + 1) >> 1;
     uint8_t *Y = (uint8_t *)malloc((size_t)dw * dh);
     uint8_t *U = (uint8_t *)malloc((size_t)dcw * dch);
@@ -724,7 +968,16 @@ size_t or_encode_frame(const uint8_t *y, int ys, const uint8_t *u, int us, const
     if (!or_scale_plane(y, ys, sw, sh, Y, dw, dw, dh, rl, bitexact_sws, lp, lp, lp, lp) &&
         !or_scale_plane(u, us, scw, sch, U, dcw, dcw, dch, rc, bitexact_sws, cp, cp, cp, cp) &&
         !or_scale_plane(v, vs, scw, sch, V, dcw, dcw, dch, rc, bitexact_sws, cp, cp, cp, cp))
-        n = or_encode_planes(Y, dw, U, dcw, V, dcw, dw, dh, qscale, sar_num, sar_den, 0, out, cap);
+        n = or_encode_planes_ex(Y, dw, U, dcw, V, dcw, dw, dh, qscale, sar_num, sar_den, 0, huff_optimal,
+                                out, cap);
     free(Y); free(U); free(V);
     return n;
+}
+
+size_t or_encode_frame(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                       int sw, int sh, int dw, int dh, int in_full_range, int qscale,
+                       int sar_num, int sar_den, int bitexact_sws, uint8_t *out, size_t cap)
+{
+    return or_encode_frame_ex(y, ys, u, us, v, vs, sw, sh, dw, dh, in_full_range, qscale, sar_num,
+                              sar_den, bitexact_sws, 0, out, cap);
 }

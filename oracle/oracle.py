@@ -51,6 +51,11 @@ def lib():
         L.or_encode_frame.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, C.c_int] + [C.c_int] * 9 + \
             [u8p, C.c_size_t]
         L.or_encode_frame.restype = C.c_size_t
+        L.or_encode_frame_ex.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, C.c_int] + [C.c_int] * 10 + \
+            [u8p, C.c_size_t]
+        L.or_encode_frame_ex.restype = C.c_size_t
+        L.or_huff_optimal.argtypes = [C.POINTER(C.c_uint32), u8p, u8p]
+        L.or_huff_optimal.restype = C.c_int
         _lib = L
     return _lib
 
@@ -167,17 +172,31 @@ def scale_plane(src, dst_w, dst_h, range_mode=0, bitexact=True, chroma=False):
 
 
 def encode_frame(y, u, v, dst_w=None, dst_h=None, full_range=False, qscale=5, sar=(1, 1),
-                 bitexact_sws=True) -> bytes:
-    """Whole worker path for one frame: [bicubic resize] + tv->pc + mjpeg encode."""
+                 bitexact_sws=True, huffman="default") -> bytes:
+    """Whole worker path for one frame: [bicubic resize] + tv->pc + mjpeg encode with
+    -huffman default (Annex K tables) or optimal (per-frame tables, mjpegenc_huffman.c)."""
+    if huffman not in ("default", "optimal"):
+        raise ValueError(huffman)
     y, u, v = _planes(y, u, v)
     sh, sw = y.shape
     dw = sw if dst_w is None else dst_w
     dh = sh if dst_h is None else dst_h
     out = np.zeros(_cap(dw, dh), np.uint8)
-    n = lib().or_encode_frame(_p(y, C.c_uint8), y.strides[0], _p(u, C.c_uint8), u.strides[0],
-                              _p(v, C.c_uint8), v.strides[0], sw, sh, dw, dh, int(bool(full_range)),
-                              int(qscale), int(sar[0]), int(sar[1]), int(bool(bitexact_sws)),
-                              _p(out, C.c_uint8), out.size)
+    n = lib().or_encode_frame_ex(_p(y, C.c_uint8), y.strides[0], _p(u, C.c_uint8), u.strides[0],
+                                 _p(v, C.c_uint8), v.strides[0], sw, sh, dw, dh,
+                                 int(bool(full_range)), int(qscale), int(sar[0]), int(sar[1]),
+                                 int(bool(bitexact_sws)), int(huffman == "optimal"),
+                                 _p(out, C.c_uint8), out.size)
     if n == 0:
-        raise RuntimeError("or_encode_frame failed")
+        raise RuntimeError("or_encode_frame_ex failed")
     return out[:n].tobytes()
+
+
+def huff_optimal(counts):
+    """BITS[1..16] and HUFFVAL of -huffman optimal for one table's 256 symbol counts
+    (ff_mjpeg_encode_huffman_close)."""
+    c = np.ascontiguousarray(np.asarray(counts, dtype=np.uint32).reshape(256))
+    bits = np.zeros(17, np.uint8)
+    vals = np.zeros(256, np.uint8)
+    n = lib().or_huff_optimal(_p(c, C.c_uint32), _p(bits, C.c_uint8), _p(vals, C.c_uint8))
+    return bits, vals[:n].copy()
