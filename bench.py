@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path named by BASELINE.json: 4K yuv420p MJPEG q=5 segment encode
-(configs[1]: "4K60 60 s testsrc2 yuv420p MJPEG q=5 on one MI355X").
+(configs[1]: "4K60 60 s testsrc2 yuv420p MJPEG q=5 on one MI355X").  `--workload` selects
+the other BASELINE configs at their own segment sizes (c1 1080p with FFmpeg's default
+-huffman optimal, c4 4K->1080p bicubic q=3, c5 8K yuvj420p 0.5 s segments); the default
+run (no flags) is configs[1], the line the driver records.
 
 A step = one 2-second segment (120 frames of 3840x2160 yuv420p) encoded on one GPU,
 frames already resident in HBM (a pool of distinct synthetic testsrc2-like frames
@@ -22,18 +25,33 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-W, H, Q, SEG = 3840, 2160, 5, 120
 METRIC = "encoded frames/sec (node), 4K yuv420p MJPEG q=5 at 1/2/4/8 GPUs; HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# BASELINE.json configs: (src W, H, dst W, H, q, frames per segment, yuvj420p input, huffman, text)
+WORKLOADS = {
+    "c2": (3840, 2160, 3840, 2160, 5, 120, False, "default",
+           "4K60 testsrc2 yuv420p MJPEG q=5 (BASELINE configs[1]); step = one 2 s segment"),
+    "c1": (1920, 1080, 1920, 1080, 5, 250, False, "optimal",
+           "1080p30 testsrc2 yuv420p MJPEG q=5, FFmpeg's default -huffman optimal (BASELINE "
+           "configs[0] profile + -dct int -bitexact); step = one 250-frame (keyint) segment"),
+    "c4": (3840, 2160, 1920, 1080, 3, 120, False, "default",
+           "4K->1080p bicubic scale + MJPEG q=3 (BASELINE configs[3]); step = one 2 s segment"),
+    "c5": (7680, 4320, 7680, 4320, 5, 15, True, "default",
+           "8K30 yuvj420p MJPEG q=5, 0.5 s segments (BASELINE configs[4]); step = one segment"),
+}
+W, H, DW, DH, Q, SEG, FULL, HUFF, WTEXT = WORKLOADS["c2"]
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    p.add_argument("--huffman", choices=["default", "optimal"], default=None)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--pool", type=int, default=480, help="distinct resident frames per GPU")
-    p.add_argument("--seg", type=int, default=SEG)
+    p.add_argument("--seg", type=int, default=None)
     p.add_argument("--cpu-sample-frames", type=int, default=96)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_encode_4k_q5.json"),
@@ -56,7 +74,8 @@ def cpu_baseline(nframes: int):
         sizes = pool.map(_cpu_encode, range(nframes))
         dt = time.perf_counter() - t0
     return {"value": nframes / dt, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"{nframes} frames 3840x2160 yuv420p q=5 (testsrc2-like, 8 distinct), "
+            "sample": f"{nframes} frames {W}x{H}{'->%dx%d' % (DW, DH) if (DW, DH) != (W, H) else ''} "
+                      f"{'yuvj420p' if FULL else 'yuv420p'} q={Q} -huffman {HUFF} (testsrc2-like, 8 distinct), "
                       f"oracle/mjpeg_oracle.c (C restatement of FFmpeg's mjpeg+swscale path), "
                       f"{cores} processes, {dt:.1f} s wall",
             "mean_jpeg_bytes": float(sum(sizes) / len(sizes))}
@@ -69,7 +88,7 @@ def _cpu_init():
     global _CPU_FRAMES
     from ffmpeg_distributed_amd.testsrc import testsrc2_i420
     from ffmpeg_distributed_amd.encoder import split_i420
-    _CPU_FRAMES = [split_i420(testsrc2_i420(W, H, t), W, H) for t in range(0, 8)]
+    _CPU_FRAMES = [split_i420(testsrc2_i420(W, H, t, full_range=FULL), W, H) for t in range(0, 8)]
 
 
 def _cpu_warm(_):
@@ -81,11 +100,18 @@ def _cpu_warm(_):
 def _cpu_encode(i):
     import oracle
     y, u, v = _CPU_FRAMES[i % len(_CPU_FRAMES)]
-    return len(oracle.encode_frame(y, u, v, qscale=Q))
+    return len(oracle.encode_frame(y, u, v, dst_w=DW, dst_h=DH, full_range=FULL, qscale=Q,
+                                   huffman=HUFF))
 
 
 def main():
+    global W, H, DW, DH, Q, SEG, FULL, HUFF, WTEXT
     a = parse()
+    W, H, DW, DH, Q, SEG, FULL, HUFF, WTEXT = WORKLOADS[a.workload]
+    if a.huffman:
+        HUFF = a.huffman
+    if a.seg is None:
+        a.seg = SEG
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -115,16 +141,18 @@ def main():
     my_segs = segments_for_rank((a.warmup + a.steps) * world, rank, world)
     nseg_pool = max(1, min(len(my_segs), a.pool // seg))
     pool_n = nseg_pool * seg
-    fb = W * H * 3 // 2
+    fb = W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)
     pool = torch.empty((pool_n, fb), dtype=torch.uint8, device=dev)
-    gen = 20
+    gen = 20 if W * H <= 3840 * 2160 else 5
     for j in range(nseg_pool):
         for i in range(0, seg, gen):
             k = min(gen, seg - i)
-            pool[j * seg + i: j * seg + i + k] = testsrc2_i420_torch(W, H, my_segs[j] * seg + i, k, dev)
+            pool[j * seg + i: j * seg + i + k] = testsrc2_i420_torch(W, H, my_segs[j] * seg + i, k, dev,
+                                                                     full_range=FULL)
     torch.cuda.synchronize()
 
-    enc = MjpegEncoder(local, W, H, qscale=Q, max_batch=seg, timing=True)
+    enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg, timing=True,
+                       huffman=HUFF)
     bytes_out = []
 
     def step(s):
@@ -146,15 +174,19 @@ def main():
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
 
     # Roofline of the dominant kernel (k_encode): algorithmic bytes per launch =
-    # (input planes 12,441,600 B + JPEG bytes written) x frames per launch.
+    # (input planes 12,441,600 B at 4K + JPEG bytes written) x frames per launch.
+    # With -vf scale the input planes are the scaled frame's (k_scale reads the source and
+    # writes them; its own line is in kernel_ms_per_step).
     enc_ms = kt["encode"]
-    alg_bytes = (fb + mean_jpeg) * seg
+    efb = DW * DH + 2 * ((DW + 1) // 2) * ((DH + 1) // 2)
+    alg_bytes = (efb + mean_jpeg) * seg
     achieved = alg_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms > 0 else 0.0
     traffic = None
     try:
         with open(a.pmc) as f:
             pm = json.load(f)
-        if pm.get("workload", {}).get("frames_per_launch") == seg:
+        if pm.get("workload", {}).get("frames_per_launch") == seg and a.workload == "c2" and \
+                HUFF == "default":
             traffic = pm.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -181,11 +213,11 @@ def main():
             "dtype": "u8",
             "data": "synthetic: testsrc2-like generator, frames resident in HBM "
                     f"({pool_n} distinct per GPU), output packed in HBM",
-            "config": {"workload": "4K60 testsrc2 yuv420p MJPEG q=5 (BASELINE configs[1]); "
-                                   "step = one 2 s segment", "width": W, "height": H,
-                       "qscale": Q, "frames_per_step": seg, "global_batch": seg * world,
-                       "parallelism": f"segment-dp{world}",
-                       "profile": "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact"},
+            "config": {"workload": WTEXT, "width": W, "height": H, "dst_width": DW,
+                       "dst_height": DH, "qscale": Q, "frames_per_step": seg,
+                       "global_batch": seg * world, "parallelism": f"segment-dp{world}",
+                       "profile": (f"-vf scale={DW}:{DH}:flags=bicubic " if (DW, DH) != (W, H) else "")
+                       + f"-c:v mjpeg -q:v {Q} -dct int -huffman {HUFF} -bitexact"},
             "roofline": {"bound": "hbm", "kernel": "k_encode",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

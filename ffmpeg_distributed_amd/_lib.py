@@ -24,8 +24,9 @@ MJG_F_TIMING = 1
 MJG_F_DEBUG_COEFS = 2
 MJG_F_SWS_NO_BITEXACT = 4
 MJG_F_COM_ITU601 = 8
+MJG_F_HUFFMAN_OPTIMAL = 16
 
-KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write")
+KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write", "huff")
 MJG_NUM_KERNELS = len(KERNEL_NAMES)
 
 # Every symbol include/mjgpu.h declares (checked by tests/test_abi.py).

@@ -46,7 +46,7 @@ struct ByteWriter {
 };
 
 std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sar_num, int sar_den,
-                                  bool com_itu601) {
+                                  bool com_itu601, size_t *dht_pos = nullptr, size_t *dht_end = nullptr) {
   ByteWriter o;
   o.u16(0xFFD8);
   if (sar_num > 0 && sar_den > 0) {
@@ -69,6 +69,7 @@ std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sa
   o.u16(2 + 65);
   o.u8(0x00);
   for (int i = 0; i < 64; i++) o.u8(mprime[kZigzag[i]]);
+  if (dht_pos) *dht_pos = o.b.size();
   o.u16(0xFFC4);
   const size_t len_at = o.b.size();
   o.u16(0);
@@ -88,6 +89,7 @@ std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sa
   const size_t dht_len = o.b.size() - len_at;
   o.b[len_at] = (uint8_t)(dht_len >> 8);
   o.b[len_at + 1] = (uint8_t)dht_len;
+  if (dht_end) *dht_end = o.b.size();
   o.u16(0xFFC0);
   o.u16(17);
   o.u8(8);
@@ -151,6 +153,11 @@ struct mjg_ctx {
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
+  // -huffman optimal
+  bool optimal = false;
+  size_t dht_pos = 0, dht_end = 0;
+  uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;
+  uint8_t *d_dht = nullptr;
   int16_t *d_dbg = nullptr;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
 
@@ -174,7 +181,8 @@ void free_ctx(mjg_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
                   c->d_chunk_off, c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
-                  c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->ps[0].hc,
+                  c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->d_hist, c->d_ftabs,
+                  c->d_dht_nval, c->d_hdr_lens, c->d_dht, c->ps[0].hc,
                   c->ps[0].vc, c->ps[0].hp, c->ps[0].vp, c->ps[1].hc, c->ps[1].vc, c->ps[1].hp,
                   c->ps[1].vp};
   for (void *p : ptrs)
@@ -280,7 +288,9 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     c->mprime[i] = (uint8_t)v;
     c->qmat[i] = (int32_t)((2ull << 21) / (uint64_t)(16 * v));
   }
-  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0);
+  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0,
+                        &c->dht_pos, &c->dht_end);
+  c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
@@ -319,6 +329,11 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096);
   if ((rc = dmalloc(&c->d_out, c->out_cap))) return rc;
   if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
+  if (c->optimal &&
+      ((rc = dmalloc(&c->d_hist, B * kFrameTabWords)) || (rc = dmalloc(&c->d_ftabs, B * kFrameTabWords)) ||
+       (rc = dmalloc(&c->d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&c->d_dht_nval, B * 4)) ||
+       (rc = dmalloc(&c->d_hdr_lens, B))))
+    return rc;
   if (g.debug_coefs && (rc = dmalloc(&c->d_dbg, B * (size_t)g.nmcu * 6 * 64))) return rc;
 #ifdef MJG_STAMPS
   if (!c->d_dbg && (rc = dmalloc(&c->d_dbg, (size_t)1 << 22))) return rc;  // 512K stamps
@@ -351,7 +366,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // persistent k_encode grid: every CU filled with as many workgroups as fit
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true>, 64 * kWavesPerWg, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
 
   c->timing = (k.flags & MJG_F_TIMING) != 0;
@@ -373,16 +388,32 @@ int launch_write(mjg_ctx *c, int n) {
   HIP_TRY(hipMemsetAsync(c->d_status, 0, 4, c->stream));
   tmark(c, MJG_K_WRITE, 0);
   k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
-                                       (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status);
+                                       (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status,
+                                       c->optimal ? c->d_hdr_lens : nullptr, (int)c->dht_pos,
+                                       (int)c->dht_end, c->d_dht, c->d_dht_nval);
   k_write<<<(ngroups + 3) / 4, 256, 0, c->stream>>>(
       c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
-      c->d_frame_offsets, (int)c->hdr.size(), g.nchunks, gpf, ngroups, c->d_out, (uint64_t)c->out_cap);
+      c->d_frame_offsets, (int)c->hdr.size(), c->optimal ? c->d_hdr_lens : nullptr, g.nchunks, gpf,
+      ngroups, c->d_out, (uint64_t)c->out_cap);
   tmark(c, MJG_K_WRITE, 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->h_sizes, c->d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
                          c->stream));
   HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, c->stream));
   return MJG_OK;
+}
+
+template <int MODE>
+void launch_encode(mjg_ctx *c, const uint8_t *enc_in, int wgs, int ntasks) {
+  const EncGeom &g = c->geom;
+  if (g.range_convert)
+    k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
+        enc_in, g, c->d_tabs, c->d_scratch, c->d_chunk_bits, c->d_dbg, c->d_work, ntasks, c->d_hist,
+        c->d_ftabs);
+  else
+    k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
+        enc_in, g, c->d_tabs, c->d_scratch, c->d_chunk_bits, c->d_dbg, c->d_work, ntasks, c->d_hist,
+        c->d_ftabs);
 }
 
 }  // namespace
@@ -466,15 +497,22 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     HIP_TRY(hipGetLastError());
     enc_in = c->d_scaled;
   }
-  tmark(c, MJG_K_ENCODE, 0);
   const int ntasks = g.nchunks * n;
   const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
-  if (g.range_convert)
-    k_encode<true><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
-                                                      c->d_chunk_bits, c->d_dbg, c->d_work, ntasks);
+  if (c->optimal) {  // pass 1: symbol counts per frame, then the frame's tables
+    tmark(c, MJG_K_HUFF, 0);
+    HIP_TRY(hipMemsetAsync(c->d_hist, 0, (size_t)n * kFrameTabWords * 4, c->stream));
+    launch_encode<kCount>(c, enc_in, wgs, ntasks);
+    HIP_TRY(hipMemsetAsync(c->d_work, 0, 4, c->stream));  // batch counter for pass 2
+    k_huff_build<<<n * 4, 64, 0, c->stream>>>(c->d_hist, c->d_ftabs, c->d_dht, c->d_dht_nval);
+    tmark(c, MJG_K_HUFF, 1);
+    HIP_TRY(hipGetLastError());
+  }
+  tmark(c, MJG_K_ENCODE, 0);
+  if (c->optimal)
+    launch_encode<kEmitFrame>(c, enc_in, wgs, ntasks);
   else
-    k_encode<false><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(enc_in, g, c->d_tabs, c->d_scratch,
-                                                      c->d_chunk_bits, c->d_dbg, c->d_work, ntasks);
+    launch_encode<kEmitDefault>(c, enc_in, wgs, ntasks);
   tmark(c, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_BITS, 0);
@@ -490,8 +528,10 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_FF, 0);
+  // optimal: header = default header - its 348 table values + the frame's
   k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
-                                       gpf, (int)c->hdr.size());
+                                       gpf, (int)c->hdr.size(), c->optimal ? c->d_dht_nval : nullptr,
+                                       (int)c->hdr.size() - 348, c->d_hdr_lens);
   tmark(c, MJG_K_SCAN_FF, 1);
   HIP_TRY(hipGetLastError());
   int rc = launch_write(c, n);
@@ -524,6 +564,7 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
     if (c->timing) {
       for (int k = 0; k < MJG_NUM_KERNELS; k++) {
         if (k == MJG_K_SCALE && !c->scale) continue;
+        if (k == MJG_K_HUFF && !c->optimal) continue;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, c->ev[k][0], c->ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
       }

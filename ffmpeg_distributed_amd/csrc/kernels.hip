@@ -154,10 +154,23 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
+// Symbol -> code lookups shared by the emitting sinks: tables hold (len << 16) | code.
+#define MJG_SINK_SYMBOLS                                                              \
+  const uint32_t *act, *dct;                                                          \
+  __device__ __forceinline__ void dc(int cat, uint32_t mant) {                        \
+    const uint32_t e = dct[cat];                                                      \
+    emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);                        \
+  }                                                                                   \
+  __device__ __forceinline__ void ac(int sym, int cat, uint32_t mant) {               \
+    const uint32_t e = act[sym];                                                      \
+    emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);                        \
+  }
+
 // Second emission pass of a block longer than RegSink's 4 words: bits at the block's
 // chunk offset, interior words stored to the slot, first/last word kept for the opener
 // logic of the pack step (k_encode).
 struct SlotSink {
+  MJG_SINK_SYMBOLS
   uint64_t acc;
   int nacc;          // bits held in acc (< 32 between emits)
   uint32_t widx;     // chunk-relative index of the word being filled
@@ -194,6 +207,7 @@ __device__ __forceinline__ int dc_cat(int diff) {
 // First emission pass: the block's bits left-aligned in up to 4 register words (a
 // block's offset in the chunk is not known yet); counts every bit even past 4 words.
 struct RegSink {
+  MJG_SINK_SYMBOLS
   uint64_t acc = 0;
   int nacc = 0;
   uint32_t bits = 0, nw = 0;
@@ -255,14 +269,11 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const in
 // testsrc2 4K q5, so the loop is short.)
 template <class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
-                                           const uint32_t *ac, const uint32_t *dc,
                                            const uint8_t *zz, const int *m2, const int *qc,
                                            Sink &sink) {
   {
     const int cat = dc_cat(diff);
-    const uint32_t e = dc[cat];
-    const uint32_t mant = (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << cat) - 1u);
-    sink.emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);
+    sink.dc(cat, (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << cat) - 1u));
   }
   int prev = 0;
   while (cand) {
@@ -273,21 +284,25 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
     int run = k - prev - 1;
     prev = k;
     while (run >= 16) {
-      const uint32_t zrl = ac[0xf0];
-      sink.emit(zrl & 0xffffu, (int)(zrl >> 16));
+      sink.ac(0xf0, 0, 0u);  // ZRL
       run -= 16;
     }
     const int a = v < 0 ? -v : v;
     const int cat = 32 - __clz(a);
-    const uint32_t e = ac[((run & 15) << 4) | cat];
-    const uint32_t mant = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u);
-    sink.emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);
+    sink.ac(((run & 15) << 4) | cat, cat, (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u));
   }
-  if (prev != 63) {
-    const uint32_t eob = ac[0];
-    sink.emit(eob & 0xffffu, (int)(eob >> 16));
-  }
+  if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB
 }
+
+// -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
+// (layout of the table block: AC luma 0-255, AC chroma 256-511, DC luma 512-527,
+// DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.
+struct CountSink {
+  uint32_t *hac, *hdc;
+  __device__ __forceinline__ void dc(int cat, uint32_t) { atomicAdd(&hdc[cat], 1u); }
+  __device__ __forceinline__ void ac(int sym, int, uint32_t) { atomicAdd(&hac[sym], 1u); }
+  __device__ __forceinline__ void finish() {}
+};
 
 // Raw 8x8 block as 8 little-endian row words.  fetch_rows issues the 8-byte row loads
 // for interior blocks (the prefetch path, 16 VGPRs) and returns false for blocks that
@@ -397,11 +412,18 @@ __device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, boo
   return lane >= 58 ? d : 128;
 }
 
-template <bool RC>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
+// MODE: kEmitDefault (-huffman default, Annex K tables), kCount (-huffman optimal pass 1:
+// per-frame symbol histograms into hist[frame][544]), kEmitFrame (-huffman optimal pass 2:
+// the frame's own tables from ftabs[frame][544], built by k_huff_build).
+constexpr int kEmitDefault = 0, kCount = 1, kEmitFrame = 2;
+constexpr int kFrameTabWords = 544;  // AC luma, AC chroma, DC luma, DC chroma (table block layout)
+
+template <bool RC, int MODE>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
-    int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks) {
+    int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
+    uint32_t *__restrict__ hist, const uint32_t *__restrict__ ftabs) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
@@ -410,6 +432,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ __attribute__((aligned(16))) int s_m2[72];       // pass-2 dot rows + per-row constant
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
+  // per wave: the current frame's histogram (kCount) or code tables (kEmitFrame)
+  __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
@@ -423,6 +447,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   }
   if (tid < 8) s_m2[64 + tid] = kPass2Add[tid];
   uint32_t *s_pk = s_pk_all[wave];
+  uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
+  if (MODE == kCount)
+    for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
+  int aux_frame = -1;  // frame whose histogram / tables s_aux holds (wave-uniform)
   __syncthreads();  // tables visible; the only workgroup barrier
 
   const int nwaves = gridDim.x * kWavesPerWg;
@@ -644,10 +672,44 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const int diff = dc - pred;
     carry = dc;
 
+    if (MODE != kEmitDefault && cur_frame != aux_frame) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS traffic is done
+      if (MODE == kCount) {  // flush the previous frame's counts
+        if (aux_frame >= 0)
+          for (int i = lane; i < kFrameTabWords; i += 64) {
+            const uint32_t v = s_aux[i];
+            if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
+            s_aux[i] = 0;
+          }
+      } else {
+        for (int i = lane; i < kFrameTabWords; i += 64)
+          s_aux[i] = ftabs[(size_t)cur_frame * kFrameTabWords + i];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      aux_frame = cur_frame;
+    }
+    if (MODE == kCount) {
+      if (cur_active) {
+        CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16};
+        emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
+      }
+      if (tn < 0) break;
+      if (new_batch) {
+        carry = carry_finish(crow, chunk, lane, rc);
+        tend = min(tn + kBatch, ntasks);
+        if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
+      }
+      t = tn;
+      continue;
+    }
+    const uint32_t *act = MODE == kEmitFrame ? s_aux + tab * 256 : s_ac + tab * 256;
+    const uint32_t *dct = MODE == kEmitFrame ? s_aux + 512 + tab * 16 : s_dc + tab * 16;
     RegSink q;
+    q.act = act;
+    q.dct = dct;
 #if MJG_ABLATE == 0 || MJG_ABLATE == 4
     if (cur_active) {
-      emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, q);
+      emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
       q.finish();
     }
 #else
@@ -687,6 +749,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
         }
       } else {  // long block: re-emit, interior words straight to the slot
         SlotSink sink;
+        sink.act = act;
+        sink.dct = dct;
         sink.acc = 0;
         sink.nacc = (int)sft;
         sink.widx = fw;
@@ -695,7 +759,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
         sink.slot = slot;
         sink.head = 0;
         sink.tail = 0;
-        emit_block(s_pk + lane, mask, diff, s_ac + tab * 256, s_dc + tab * 16, s_zz, s_m2, s_qc, sink);
+        emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, sink);
         sink.finish();
         head = sink.head;
         tail = sink.tail;
@@ -721,6 +785,237 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     }
     t = tn;
   }
+  if (MODE == kCount && aux_frame >= 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < kFrameTabWords; i += 64) {
+      const uint32_t v = s_aux[i];
+      if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
+    }
+  }
+}
+
+// ------------------------------------------------------------- k_huff_build
+// -huffman optimal tables of one (frame, table) per 64-thread workgroup, restating
+// libavcodec/mjpegenc_huffman.c (ff_mjpeg_encode_huffman_close ->
+// ff_mjpegenc_huffman_compute_bits) and libavutil/qsort.h AV_QSORT exactly (see
+// oracle/mjpeg_oracle.c for the CPU restatement this is tested against):
+//   1. nonzero counts in ascending symbol order + the dummy symbol 256 with count 0;
+//   2. AV_QSORT by count (lane 0; its tie order decides which equal-count symbols get
+//      the longer codes, so it is reproduced step for step);
+//   3. package-merge lists X_0..X_15 (X_t = merge of the leaves and the pairwise packages
+//      of X_{t-1}, a package first on equal weight), merged in parallel by rank: a leaf
+//      lands after the packages of weight <= its own, a package after the leaves lighter
+//      than it; only each entry's weight and leaf/package tag are kept;
+//   4. X_16 = packages of X_15; its first m = min(n-1, |X_16|) entries are selected, which
+//      selects a prefix of every X_t: s_15 = 2m, and s_{t-1} = 2 * (packages among the
+//      first s_t entries of X_t).  A leaf's code length is the number of lists whose
+//      selected prefix holds it;
+//   5. BITS/HUFFVAL ordered by (length, symbol) and canonical codes
+//      (ff_mjpeg_build_huffman_codes).
+// Table t: 0 DC luma, 1 DC chroma, 2 AC luma, 3 AC chroma.  Outputs: ftabs[f][544]
+// ((len << 16) | code, table block layout), dht[f][t][kDhtSlot] (BITS[1..16] then
+// HUFFVAL) and dht_nval[f][t].
+constexpr int kDhtSlot = 16 + 256;
+constexpr int kPmMax = 520;  // >= 257 leaves + 257 packages
+
+__device__ void av_qsort_pairs(int *val, int *key, int num) {
+  int stack[64][2];
+  int sp = 1;
+  stack[0][0] = 0;
+  stack[0][1] = num - 1;
+#define MJG_SWAP(a, b)                     \
+  do {                                     \
+    const int ia_ = (a), ib_ = (b);        \
+    const int tk_ = key[ia_], tv_ = val[ia_]; \
+    key[ia_] = key[ib_];                   \
+    val[ia_] = val[ib_];                   \
+    key[ib_] = tk_;                        \
+    val[ib_] = tv_;                        \
+  } while (0)
+#define MJG_CMP(a, b) (key[a] - key[b])
+  while (sp) {
+    int start = stack[--sp][0];
+    int end = stack[sp][1];
+    while (start < end) {
+      if (start < end - 1) {
+        bool checksort = false;
+        int right = end - 2, left = start + 1;
+        int mid = start + ((end - start) >> 1);
+        if (MJG_CMP(start, end) > 0) {
+          if (MJG_CMP(end, mid) > 0)
+            MJG_SWAP(start, mid);
+          else
+            MJG_SWAP(start, end);
+        } else {
+          if (MJG_CMP(start, mid) > 0)
+            MJG_SWAP(start, mid);
+          else
+            checksort = true;
+        }
+        if (MJG_CMP(mid, end) > 0) {
+          MJG_SWAP(mid, end);
+          checksort = false;
+        }
+        if (start == end - 2) break;
+        MJG_SWAP(end - 1, mid);
+        while (left <= right) {
+          while (left <= right && MJG_CMP(left, end - 1) < 0) left++;
+          while (left <= right && MJG_CMP(right, end - 1) > 0) right--;
+          if (left <= right) {
+            MJG_SWAP(left, right);
+            left++;
+            right--;
+          }
+        }
+        MJG_SWAP(end - 1, left);
+        if (checksort && (mid == left - 1 || mid == left)) {
+          mid = start;
+          while (mid < end && MJG_CMP(mid, mid + 1) <= 0) mid++;
+          if (mid == end) break;
+        }
+        if (end - left < left - start) {
+          stack[sp][0] = start;
+          stack[sp++][1] = right;
+          start = left + 1;
+        } else {
+          stack[sp][0] = left + 1;
+          stack[sp++][1] = end;
+          end = right;
+        }
+      } else {
+        if (MJG_CMP(start, end) > 0) MJG_SWAP(start, end);
+        break;
+      }
+    }
+  }
+#undef MJG_SWAP
+#undef MJG_CMP
+}
+
+__global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ hist,
+                                                   uint32_t *__restrict__ ftabs,
+                                                   uint8_t *__restrict__ dht,
+                                                   uint32_t *__restrict__ dht_nval) {
+  __shared__ int s_val[260], s_key[260];   // leaves: symbol, count (sorted by count)
+  __shared__ int s_w[2][kPmMax];            // weights of X_{t-1} / X_t
+  __shared__ uint8_t s_tag[16][kPmMax];     // 1 = leaf entry of X_t
+  __shared__ int s_pre[17];                 // leaves in the selected prefix of X_t
+  __shared__ int s_len[256];                // code length per symbol
+  __shared__ uint32_t s_mask[17][8];        // symbols per length (bitmap)
+  __shared__ int s_bits[17], s_off[17], s_first[17];
+  __shared__ int s_n;
+  const int f = blockIdx.x >> 2, t = blockIdx.x & 3, lane = threadIdx.x;
+  const uint32_t *h = hist + (size_t)f * kFrameTabWords + (t < 2 ? 512 + 16 * t : 256 * (t - 2));
+  const int nb = t < 2 ? 16 : 256;
+
+  // 1. compaction in ascending symbol order
+  int n = 0;
+  for (int base = 0; base < nb; base += 64) {
+    const int sym = base + lane;
+    const uint32_t c = sym < nb ? h[sym] : 0u;
+    const uint64_t m = __ballot(c != 0);
+    const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+    if (c) {
+      s_val[pos] = sym;
+      s_key[pos] = (int)c;
+    }
+    n += __popcll(m);
+  }
+  for (int i = lane; i < 256; i += 64) s_len[i] = 0;
+  for (int i = lane; i < 17 * 8; i += 64) (&s_mask[0][0])[i] = 0;
+  if (lane == 0) {
+    s_val[n] = 256;
+    s_key[n] = 0;
+    av_qsort_pairs(s_val, s_key, n + 1);  // 2.
+  }
+  __syncthreads();
+  const int size = n + 1;
+
+  // 3. forward lists
+  int len_prev = 0;  // |X_{t-1}|
+  for (int lt = 0; lt < 16; lt++) {
+    int *prev = s_w[(lt + 1) & 1], *cur = s_w[lt & 1];
+    const int np = len_prev >> 1;
+    for (int i = lane; i < size; i += 64) {  // leaf i: after the packages with weight <= key
+      const int key = s_key[i];
+      int lo = 0, hi = np;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (prev[2 * mid] + prev[2 * mid + 1] <= key) lo = mid + 1; else hi = mid;
+      }
+      cur[i + lo] = key;
+      s_tag[lt][i + lo] = 1;
+    }
+    for (int j = lane; j < np; j += 64) {  // package j: after the leaves lighter than it
+      const int w = prev[2 * j] + prev[2 * j + 1];
+      int lo = 0, hi = size;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_key[mid] < w) lo = mid + 1; else hi = mid;
+      }
+      cur[j + lo] = w;
+      s_tag[lt][j + lo] = 0;
+    }
+    len_prev = size + np;
+    __syncthreads();
+  }
+  // 4. selection, backwards
+  {
+    const int m = min(size - 1, len_prev >> 1);  // X_16 = packages of X_15
+    int sel = 2 * m;                              // wave-uniform
+    for (int lt = 15; lt >= 1; lt--) {
+      int leaves = 0;
+      for (int k = lane; k < sel; k += 64) leaves += s_tag[lt][k];
+      leaves = wave_sum(leaves);
+      if (lane == 0) s_pre[lt] = leaves;
+      sel = 2 * (sel - leaves);
+    }
+    if (lane == 0) s_pre[0] = sel;
+  }
+  __syncthreads();
+  for (int i = lane; i < size; i += 64) {
+    int L = 0;
+#pragma unroll
+    for (int lt = 0; lt < 16; lt++) L += i < s_pre[lt] ? 1 : 0;
+    const int sym = s_val[i];
+    if (sym < 256 && L > 0) {
+      s_len[sym] = L;
+      atomicOr(&s_mask[L][sym >> 5], 1u << (sym & 31));
+    }
+  }
+  __syncthreads();
+  // 5. BITS / HUFFVAL by (length, symbol), canonical codes
+  if (lane == 0) {
+    int off = 0, code = 0;
+    for (int L = 1; L <= 16; L++) {
+      int c = 0;
+      for (int w = 0; w < 8; w++) c += __popc(s_mask[L][w]);
+      s_bits[L] = c;
+      s_off[L] = off;
+      s_first[L] = code;
+      off += c;
+      code = (code + c) << 1;
+    }
+    s_n = off;
+  }
+  __syncthreads();
+  uint8_t *d = dht + ((size_t)f * 4 + t) * kDhtSlot;
+  if (lane >= 1 && lane <= 16) d[lane - 1] = (uint8_t)s_bits[lane];
+  uint32_t *ft = ftabs + (size_t)f * kFrameTabWords + (t < 2 ? 512 + 16 * t : 256 * (t - 2));
+  for (int sym = lane; sym < nb; sym += 64) {
+    const int L = s_len[sym];
+    uint32_t e = 0;
+    if (L) {
+      int rank = 0;
+      for (int w = 0; w < (sym >> 5); w++) rank += __popc(s_mask[L][w]);
+      rank += __popc(s_mask[L][sym >> 5] & ((1u << (sym & 31)) - 1u));
+      const int k = s_off[L] + rank;
+      d[16 + k] = (uint8_t)sym;
+      e = ((uint32_t)L << 16) | (uint32_t)(s_first[L] + rank);
+    }
+    ft[sym] = e;
+  }
+  if (lane == 0) dht_nval[(size_t)f * 4 + t] = (uint32_t)s_n;
 }
 
 // --------------------------------------------------------------- block scan
@@ -881,24 +1176,40 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
 }
 
 // Per frame: exclusive scan of the chunk groups' 0xFF counts -> stuffed frame size.
+// -huffman optimal (dht_nval != null): the header length is per frame, hdr_base plus the
+// frame's table values, stored to hdr_lens for k_frame_hdr / k_write.
 __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ group_ff,
                                                   uint32_t *__restrict__ ff_off,
                                                   const uint32_t *__restrict__ frame_bits,
                                                   uint64_t *__restrict__ frame_size, int ngroups_per_frame,
-                                                  int hdr_len) {
+                                                  int hdr_len, const uint32_t *__restrict__ dht_nval,
+                                                  int hdr_base, uint32_t *__restrict__ hdr_lens) {
   const int f = blockIdx.x;
   const size_t g0 = (size_t)f * ngroups_per_frame;
   const uint32_t t = block_excl_scan(group_ff + g0, ff_off + g0, ngroups_per_frame);
-  if (threadIdx.x == 0) frame_size[f] = (uint64_t)hdr_len + ((frame_bits[f] + 7) >> 3) + t + 2;
+  if (threadIdx.x == 0) {
+    uint32_t hl = (uint32_t)hdr_len;
+    if (dht_nval) {
+      hl = (uint32_t)hdr_base + dht_nval[4 * f] + dht_nval[4 * f + 1] + dht_nval[4 * f + 2] +
+           dht_nval[4 * f + 3];
+      hdr_lens[f] = hl;
+    }
+    frame_size[f] = (uint64_t)hl + ((frame_bits[f] + 7) >> 3) + t + 2;
+  }
 }
 
 // One wave per frame: packed output offset (sum of the preceding frame sizes), capacity
-// check, header (SOI .. SOS) and EOI of the frame.
+// check, header (SOI .. SOS) and EOI of the frame.  -huffman optimal (hdr_lens != null):
+// the default header's bytes before and after its DHT around the frame's own DHT
+// (jpeg_table_header: one DHT, tables DC0, DC1, AC0, AC1).
 __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ frame_size,
                                                   const uint8_t *__restrict__ hdr, int hdr_len,
                                                   uint8_t *__restrict__ out, uint64_t out_cap,
                                                   uint64_t *__restrict__ frame_offsets,
-                                                  uint32_t *__restrict__ status) {
+                                                  uint32_t *__restrict__ status,
+                                                  const uint32_t *__restrict__ hdr_lens, int dht_pos,
+                                                  int dht_end, const uint8_t *__restrict__ dht,
+                                                  const uint32_t *__restrict__ dht_nval) {
   const int f = blockIdx.x, lane = threadIdx.x;
   uint64_t s = 0;
   for (int i = lane; i < f; i += 64) s += frame_size[i];
@@ -914,7 +1225,30 @@ __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ f
     return;
   }
   uint8_t *fo = out + s;
-  for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
+  if (!hdr_lens) {
+    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
+  } else {
+    const uint32_t *nv = dht_nval + 4 * (size_t)f;
+    const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
+    for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
+    uint8_t *o = fo + dht_pos;
+    if (lane == 0) {
+      o[0] = 0xff;
+      o[1] = 0xc4;
+      o[2] = (uint8_t)(len >> 8);
+      o[3] = (uint8_t)len;
+    }
+    o += 4;
+    for (int t = 0; t < 4; t++) {
+      const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
+      const int n = 16 + (int)nv[t];
+      if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
+      for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
+      o += 1 + n;
+    }
+    const int tail = hdr_len - dht_end;
+    for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
+  }
   if (lane == 0) {
     fo[fsize - 2] = 0xff;
     fo[fsize - 1] = 0xd9;
@@ -928,14 +1262,15 @@ __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
     const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
     const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
-    const uint64_t *__restrict__ frame_offsets, int hdr_len, int nchunks, int ngroups_per_frame,
-    int ngroups, uint8_t *__restrict__ out, uint64_t out_cap) {
+    const uint64_t *__restrict__ frame_offsets, int hdr_len, const uint32_t *__restrict__ hdr_lens,
+    int nchunks, int ngroups_per_frame, int ngroups, uint8_t *__restrict__ out, uint64_t out_cap) {
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (gi >= ngroups) return;
   const GroupWords g = group_words(chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
   const uint64_t foff = frame_offsets[g.f];
   if (foff + frame_size[g.f] > out_cap) return;  // k_frame_hdr flagged the overflow
-  uint8_t *base = out + foff + hdr_len + 4 * (size_t)g.k0 + ff_off[gi];
+  const uint32_t hl = hdr_lens ? hdr_lens[g.f] : (uint32_t)hdr_len;
+  uint8_t *base = out + foff + hl + 4 * (size_t)g.k0 + ff_off[gi];
   uint32_t carry = 0;
   for (uint32_t kb = g.k0; kb < g.k1; kb += 64) {
     const uint32_t k = kb + lane;

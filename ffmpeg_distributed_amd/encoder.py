@@ -1,7 +1,7 @@
 """GPU MJPEG encoder: the per-segment encode that the reference's worker runs
 (`ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:`,
 ffmpeg_distributed.py:131-141), restricted to the profile
-`[-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int -huffman default -bitexact`.
+`[-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int [-huffman default|optimal] -bitexact`.
 
 Host-side wrapper over libmjgpu.so; frames are packed I420 (yuv420p / yuvj420p), i.e.
 what `ffmpeg -f rawvideo -pix_fmt yuv420p` writes.  No CPU fallback.
@@ -41,7 +41,8 @@ class MjpegEncoder:
     def __init__(self, device: int, src_w: int, src_h: int, dst_w: Optional[int] = None,
                  dst_h: Optional[int] = None, full_range: bool = False, qscale: int = 5,
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
-                 debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False):
+                 debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
+                 huffman: str = "default"):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -57,6 +58,11 @@ class MjpegEncoder:
             flags |= _lib.MJG_F_SWS_NO_BITEXACT
         if com_itu601:
             flags |= _lib.MJG_F_COM_ITU601
+        if huffman == "optimal":
+            flags |= _lib.MJG_F_HUFFMAN_OPTIMAL
+        elif huffman != "default":
+            raise ValueError(f"huffman {huffman!r}")
+        self.huffman = huffman
         sar = sar or (0, 0)
         cfg = MjgConfig(self.src_w, self.src_h, self.dst_w, self.dst_h, int(bool(full_range)),
                         int(qscale), int(sar[0]), int(sar[1]), self.max_batch, flags)

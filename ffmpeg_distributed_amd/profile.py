@@ -2,8 +2,8 @@
 :134 passes them to the worker ffmpeg) into the GPU encode profile, or report why the
 arguments fall outside it (the worker then runs the real ffmpeg unchanged).
 
-Supported profile (BASELINE north star):
-    [-vf scale=W:H[:flags=bicubic...]] -c:v mjpeg -q:v N -dct int -huffman default -bitexact
+Supported profile (BASELINE north star, plus FFmpeg's default -huffman optimal):
+    [-vf scale=W:H[:flags=bicubic...]] -c:v mjpeg -q:v N -dct int [-huffman default|optimal] -bitexact
 plus options that do not change the video bitstream: -an -sn -dn -y -threads N
 -pix_fmt yuvj420p -f matroska -map 0:v[:0].
 """
@@ -21,6 +21,7 @@ class Profile:
     q_arg: float                     # the -q:v value as given
     scale: Optional[Tuple[int, int]] = None   # -vf scale=W:H
     sws_flags: Tuple[str, ...] = ("bicubic",)
+    huffman: str = "optimal"         # mjpegenc.c "huffman" option, default optimal
 
 
 class Unsupported(ValueError):
@@ -125,11 +126,13 @@ def parse(args: Union[str, Sequence[str]]) -> Profile:
         raise Unsupported("no -q:v (rate control modes are not GPU-accelerated)")
     if dct != "int":
         raise Unsupported(f"-dct {dct!r} (only the integer jfdctint is bit-exact reproducible)")
-    if huff != "default":
-        raise Unsupported(f"-huffman {huff!r} (optimal tables: next round)")
+    if huff is None:
+        huff = "optimal"  # mjpegenc.c: the "huffman" AVOption defaults to HUFFMAN_TABLE_OPTIMAL
+    if huff not in ("default", "optimal"):
+        raise Unsupported(f"-huffman {huff!r}")
     if not bitexact:
         raise Unsupported("no -bitexact (the Lavc COM segment is build-specific)")
-    return Profile(qscale=effective_qscale(q), q_arg=q, scale=scale, sws_flags=flags)
+    return Profile(qscale=effective_qscale(q), q_arg=q, scale=scale, sws_flags=flags, huffman=huff)
 
 
 def av_reduce(num: int, den: int, max_v: int) -> Tuple[int, int]:

@@ -174,7 +174,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
                        qscale=prof.qscale, sar=sar, max_batch=BATCH,
-                       com_itu601=COM_ITU601 and not info.full_range)
+                       com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman)
     prog = Progress(stderr, info.fps, prof.qscale)
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)

@@ -43,6 +43,9 @@ extern "C" {
 #define MJG_F_COM_ITU601 8u    /* add COM "CS=ITU601" (FFmpeg builds whose CLI hands the encoder
                                   yuv420p+full-range instead of yuvj420p; mjpegenc_common.c
                                   jpeg_put_comments) */
+#define MJG_F_HUFFMAN_OPTIMAL 16u /* -huffman optimal (FFmpeg's default): per-frame Huffman tables
+                                  from the frame's symbol counts (mjpegenc_huffman.c); the
+                                  header's DHT then differs per frame */
 
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane)        */
@@ -51,7 +54,8 @@ extern "C" {
 #define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk      */
 #define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes        */
 #define MJG_K_WRITE 5          /* header + stuffed scan + EOI into packed output     */
-#define MJG_NUM_KERNELS 6
+#define MJG_K_HUFF 6           /* -huffman optimal: symbol-count pass + table build   */
+#define MJG_NUM_KERNELS 7
 
 typedef struct mjg_config {
   int32_t src_w, src_h;      /* decoded frame size (packed I420: Y, then U, then V)    */

@@ -49,12 +49,12 @@ def rand_frames(w, h, n, seed, kind="noise"):
     raise ValueError(kind)
 
 
-def oracle_frames(frames, w, h, q, full_range, dw=None, dh=None, sar=(1, 1)):
+def oracle_frames(frames, w, h, q, full_range, dw=None, dh=None, sar=(1, 1), huffman="default"):
     out = []
     for f in frames:
         y, u, v = split_i420(f, w, h)
         out.append(oracle.encode_frame(y, u, v, dst_w=dw, dst_h=dh, full_range=full_range,
-                                       qscale=q, sar=sar))
+                                       qscale=q, sar=sar, huffman=huffman))
     return out
 
 
@@ -90,6 +90,27 @@ def test_encode_matches_oracle(w, h, q, full, kind):
     ref = oracle_frames(frames, w, h, q, full)
     for i in range(n):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+@pytest.mark.parametrize("w,h,q,full,kind", CASES)
+def test_encode_huffman_optimal_matches_oracle(w, h, q, full, kind):
+    """-huffman optimal (FFmpeg's default): per-frame tables from GPU symbol counts."""
+    n = 3
+    frames = rand_frames(w, h, n, seed=w * 17 + h + q, kind=kind)
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=4, huffman="optimal") as enc:
+        got = enc.encode(frames)
+    ref = oracle_frames(frames, w, h, q, full, huffman="optimal")
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+def test_huffman_optimal_scaled_batches():
+    """optimal tables with -vf scale, ragged batches and a reused context."""
+    sw, sh, dw, dh, q = 160, 96, 80, 48, 3
+    frames = rand_frames(sw, sh, 5, seed=3, kind="smooth")
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, max_batch=3, huffman="optimal") as enc:
+        got = enc.encode(frames[:3]) + enc.encode(frames[3:])
+    assert got == oracle_frames(frames, sw, sh, q, False, dw, dh, huffman="optimal")
 
 
 @pytest.mark.parametrize("w,h,q,full", [(72, 40, 5, False), (1920, 1080, 3, True)])

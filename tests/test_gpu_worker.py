@@ -17,8 +17,12 @@ pytestmark = pytest.mark.gpu
 ARGS = "-c:v mjpeg -q:v {q} -dct int -huffman default -bitexact".split()
 
 
-def _args(q, scale=None):
+def _args(q, scale=None, huffman="default"):
     a = [x.format(q=q) for x in ARGS]
+    if huffman is None:  # no -huffman: FFmpeg's default, optimal
+        a = a[:6] + a[8:]
+    else:
+        a[7] = huffman
     return (["-vf", f"scale={scale[0]}:{scale[1]}:flags=bicubic"] if scale else []) + a
 
 
@@ -74,3 +78,15 @@ def test_worker_raw_mkv_full_range(monkeypatch):
     for i, f in enumerate(frames):
         y, u, v = split_i420(f, w, h)
         assert packets[i] == oracle.encode_frame(y, u, v, full_range=True, qscale=4, sar=(1, 1))
+
+
+@pytest.mark.parametrize("huffman", ["optimal", None])
+def test_worker_huffman_optimal(huffman, monkeypatch):
+    """-huffman optimal, explicit or by default (no -huffman, as BASELINE configs[0] runs)."""
+    w, h, n, q = 144, 80, 5, 5
+    frames = [make_testsrc(w, h, 7 + i) for i in range(n)]
+    r, packets, _ = _run(_y4m(frames, w, h), _args(q, huffman=huffman), monkeypatch, 2)
+    for i, f in enumerate(frames):
+        y, u, v = split_i420(f, w, h)
+        ref = oracle.encode_frame(y, u, v, full_range=False, qscale=q, sar=(1, 1), huffman="optimal")
+        assert packets[i] == ref, f"frame {i}"

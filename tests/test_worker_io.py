@@ -26,7 +26,16 @@ def test_profile_north_star():
     p = profile.parse(NORTH_STAR)
     assert p.scale == (1920, 1080) and p.qscale == 5 and p.sws_flags == ("bicubic",)
     p = profile.parse("-c:v mjpeg -q:v 2 -dct int -huffman default -flags +bitexact -an")
-    assert p.scale is None and p.qscale == 2
+    assert p.scale is None and p.qscale == 2 and p.huffman == "default"
+
+
+@pytest.mark.parametrize("args,huff", [
+    ("-c:v mjpeg -q:v 5 -dct int -huffman optimal -bitexact", "optimal"),
+    ("-c:v mjpeg -q:v 5 -dct int -bitexact", "optimal"),  # FFmpeg's default mode
+    ("-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact", "default"),
+])
+def test_profile_huffman_modes(args, huff):
+    assert profile.parse(args).huffman == huff
 
 
 @pytest.mark.parametrize("q,expect", [(1, 2), (2, 2), (3, 3), (5, 5), (31, 31), (40, 31), (4.5, 5), (4.4, 4), (7.9, 8)])
@@ -37,7 +46,7 @@ def test_profile_qscale_mapping(q, expect):
 
 @pytest.mark.parametrize("args", [
     "-c:v libx264 -crf 18",
-    "-c:v mjpeg -q:v 5 -dct int -huffman optimal -bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -huffman zigzag -bitexact",
     "-c:v mjpeg -q:v 5 -huffman default -bitexact",                  # default dct is not int
     "-c:v mjpeg -q:v 5 -dct int -huffman default",                   # no -bitexact
     "-c:v mjpeg -b:v 10M -dct int -huffman default -bitexact",       # rate control
