@@ -123,8 +123,7 @@ int dmalloc(T **p, size_t count) {
 
 struct PlaneScale {
   SwsFilter hf, vf;
-  int16_t *hc = nullptr, *vc = nullptr;
-  int32_t *hp = nullptr, *vp = nullptr;
+  int32_t *hcp = nullptr, *hp = nullptr, *vcp = nullptr, *vps = nullptr;
   ScaleGeom g{};
   size_t lds = 0;
   dim3 grid;
@@ -182,9 +181,9 @@ void free_ctx(mjg_ctx *c) {
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
                   c->d_chunk_off, c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
                   c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->d_hist, c->d_ftabs,
-                  c->d_dht_nval, c->d_hdr_lens, c->d_dht, c->ps[0].hc,
-                  c->ps[0].vc, c->ps[0].hp, c->ps[0].vp, c->ps[1].hc, c->ps[1].vc, c->ps[1].hp,
-                  c->ps[1].vp};
+                  c->d_dht_nval, c->d_hdr_lens, c->d_dht, c->ps[0].hcp,
+                  c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
+                  c->ps[1].vps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_sizes) (void)hipHostFree(c->h_sizes);
@@ -205,37 +204,59 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
       !make_sws_filter(sh, dh, 1 << 12, 2, bitexact, pos, pos, &p.vf))
     return set_err(MJG_E_INVALID, "scale %dx%d -> %dx%d needs swscale's cascade (unsupported)", sw,
                    sh, dw, dh);
-  // LDS extents over all tiles (positions are monotone after initFilter's reduce step).
-  int max_rows = 0, max_cols = 0;
-  for (int y0 = 0; y0 < dh; y0 += kScaleTileH) {
-    const int ye = std::min(y0 + kScaleTileH, dh);
-    max_rows = std::max(max_rows, p.vf.pos[ye - 1] + p.vf.taps - p.vf.pos[y0]);
-  }
-  for (int x0 = 0; x0 < dw; x0 += kScaleTileW) {
-    const int xe = std::min(x0 + kScaleTileW, dw);
-    max_cols = std::max(max_cols, p.hf.pos[xe - 1] + p.hf.taps - p.hf.pos[x0]);
-  }
   for (int i = 1; i < dw; i++)
     if (p.hf.pos[i] < p.hf.pos[i - 1]) return set_err(MJG_E_INVALID, "non-monotone hscale");
   for (int i = 1; i < dh; i++)
     if (p.vf.pos[i] < p.vf.pos[i - 1]) return set_err(MJG_E_INVALID, "non-monotone vscale");
+  const int ht = p.hf.taps, vt = p.vf.taps;
+  if ((ht & 3) || (vt & 1)) return set_err(MJG_E_INVALID, "filter taps %d/%d not aligned", ht, vt);
+  for (int i = 0; i < dw; i++)
+    if (p.hf.pos[i] + ht > sw) return set_err(MJG_E_INVALID, "hscale window past the row");
+  // h: coefficient pairs per output column; v: pairs starting at the even row <= pos[y],
+  // shifted by its parity and zero-padded to npv = vt/2 + 1 pairs
+  const int npv = vt / 2 + 1;
+  std::vector<int32_t> hcp((size_t)dw * (ht / 2)), vcp((size_t)dh * npv, 0), vps(dh);
+  for (int x = 0; x < dw; x++)
+    for (int k = 0; k < ht / 2; k++)
+      hcp[(size_t)x * (ht / 2) + k] = (int32_t)((uint32_t)(uint16_t)p.hf.coeff[(size_t)x * ht + 2 * k] |
+                                                ((uint32_t)(uint16_t)p.hf.coeff[(size_t)x * ht + 2 * k + 1] << 16));
+  for (int y = 0; y < dh; y++) {
+    const int r = p.vf.pos[y], par = r & 1;
+    vps[y] = r >> 1;
+    for (int k = 0; k < npv; k++) {
+      const int j0 = 2 * k - par, j1 = j0 + 1;
+      const uint16_t c0 = (j0 >= 0 && j0 < vt) ? (uint16_t)p.vf.coeff[(size_t)y * vt + j0] : 0;
+      const uint16_t c1 = (j1 >= 0 && j1 < vt) ? (uint16_t)p.vf.coeff[(size_t)y * vt + j1] : 0;
+      vcp[(size_t)y * npv + k] = (int32_t)((uint32_t)c0 | ((uint32_t)c1 << 16));
+    }
+  }
+  int max_pairs = 0, max_nw = 0;
+  for (int y0 = 0; y0 < dh; y0 += kScaleTileH) {
+    const int ye = std::min(y0 + kScaleTileH, dh);
+    max_pairs = std::max(max_pairs, vps[ye - 1] + npv - vps[y0]);
+  }
+  for (int x0 = 0; x0 < dw; x0 += kScaleTileW) {  // same formula as k_scale's window
+    const int xe = std::min(x0 + kScaleTileW, dw), cb = p.hf.pos[x0] & ~3;
+    max_nw = std::max(max_nw, ((p.hf.pos[xe - 1] + ht - cb + 3) >> 2) + 1);
+  }
   ScaleGeom &g = p.g;
-  g.htaps = p.hf.taps;
-  g.vtaps = p.vf.taps;
-  g.lds_cols = (max_cols + 15) & ~15;
-  g.lds_rows = max_rows;
-  p.lds = (size_t)g.lds_rows * g.lds_cols + (size_t)g.lds_rows * kScaleTileW * 2;
+  g.htaps = ht;
+  g.vtaps = vt;
+  g.npv = npv;
+  g.lds_pairs = max_pairs;
+  g.lds_win_words = 2 * max_pairs * max_nw;
+  p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW) * 4;
   if (p.lds > 64 * 1024)
     return set_err(MJG_E_INVALID, "scale ratio too large for one LDS tile (%zu B)", p.lds);
   p.grid = dim3((dw + kScaleTileW - 1) / kScaleTileW, (dh + kScaleTileH - 1) / kScaleTileH, 1);
   int rc;
-  if ((rc = dmalloc(&p.hc, p.hf.coeff.size())) || (rc = dmalloc(&p.hp, p.hf.pos.size())) ||
-      (rc = dmalloc(&p.vc, p.vf.coeff.size())) || (rc = dmalloc(&p.vp, p.vf.pos.size())))
+  if ((rc = dmalloc(&p.hcp, hcp.size())) || (rc = dmalloc(&p.hp, (size_t)dw)) ||
+      (rc = dmalloc(&p.vcp, vcp.size())) || (rc = dmalloc(&p.vps, (size_t)dh)))
     return rc;
-  HIP_TRY(hipMemcpy(p.hc, p.hf.coeff.data(), p.hf.coeff.size() * 2, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(p.hp, p.hf.pos.data(), p.hf.pos.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(p.vc, p.vf.coeff.data(), p.vf.coeff.size() * 2, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(p.vp, p.vf.pos.data(), p.vf.pos.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.hcp, hcp.data(), hcp.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.hp, p.hf.pos.data(), (size_t)dw * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.vcp, vcp.data(), vcp.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p.vps, vps.data(), (size_t)dh * 4, hipMemcpyHostToDevice));
   (void)c;
   return MJG_OK;
 }
@@ -491,7 +512,12 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       }
       dim3 grid = ps.grid;
       grid.z = n;
-      k_scale<<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hc, ps.hp, ps.vc, ps.vp);
+      if (sg.htaps == 8 && sg.npv == 5)  // 2:1 downscale (4K -> 1080p)
+        k_scale<8, 5><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
+      else if (sg.htaps == 4 && sg.npv == 3)  // upscale / mild downscale
+        k_scale<4, 3><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
+      else
+        k_scale<0, 0><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
     }
     tmark(c, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());

@@ -4,27 +4,39 @@
 //   hScale8To15_c: min((sum src*f) >> 7, 32767)            (14-bit coeffs)
 //   lumRangeToJpeg_c / chrRangeToJpeg_c on that int16       (tv -> pc, if requested)
 //   yuv2planeX_8_c: clip_u8(((64 << 12) + sum h*f) >> 19)  (12-bit coeffs, flat dither)
-// One workgroup = a 64 x 16 output tile: the source window is staged in LDS with
-// coalesced byte loads, the horizontal pass fills an int16 LDS tile of every source
-// row the tile's vertical taps touch, then the vertical pass writes the output.
+//
+// One workgroup = a 64 x 32 output tile (4 waves, lane = output column).
+//   load:   the tile's source window (rows x dword-aligned columns) is staged in LDS with
+//           coalesced dword loads, many in flight per thread.
+//   h-pass: wave w computes source row pairs p0+w, p0+w+4, ... of the window for its lane's
+//           column: taps funnel-shifted out of aligned LDS dwords (v_alignbit), widened to
+//           u16 pairs with v_perm and multiplied with v_dot2_i32_i16 against the column's
+//           coefficient pairs (registers).  Rows 2p and 2p+1 go to LDS as one int16 pair.
+//   v-pass: output row y reads the pairs [vps[y], vps[y] + npv) of its column and dot2s
+//           them against that row's coefficient pairs, which the host pre-shifts by the
+//           parity of the first tap row (zero-padded), so odd and even starts cost the same.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace mjg {
 
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
 constexpr int kScaleTileW = 64;
-constexpr int kScaleTileH = 16;
+constexpr int kScaleTileH = 32;
+constexpr int kScaleMaxRowsPerWave = 20;  // window rows per wave on the fast load path (2:1: 18)
 
 struct ScaleGeom {
   int sw, sh, dw, dh;            // plane sizes
   int s_stride, d_stride;
   long long s_off, d_off;        // plane offset inside a frame
   long long s_fstride, d_fstride;  // frame strides
-  int htaps, vtaps;
+  int htaps, vtaps;              // htaps multiple of 4 (filterAlign 4), vtaps even
+  int npv;                       // coefficient pairs per output row (vtaps/2 + 1)
   int range;                     // 0 none, 1 luma tv->pc, 2 chroma tv->pc
-  int lds_cols;                  // padded source-window width (multiple of 16)
-  int lds_rows;                  // max source rows any tile needs
+  int lds_pairs;                 // max row pairs any tile needs
+  int lds_win_words;             // max source-window dwords any tile needs
 };
 
 __device__ __forceinline__ int sws_range(int v, int range) {
@@ -39,51 +51,110 @@ __device__ __forceinline__ int sws_range(int v, int range) {
   return v;
 }
 
+// hScale8To15 of one source row (taps = the `htaps` bytes at byte offset `off` of an LDS
+// row), then range conversion.  Bytes are fetched as aligned dwords and funnel-shifted.
+template <int HT>  // 0: runtime htaps
+__device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const int32_t *hcp, int htaps_rt,
+                                          int range) {
+  const int htaps = HT ? HT : htaps_rt;
+  const uint32_t *q = row + (off >> 2);
+  const uint32_t sh = (uint32_t)(off & 3) * 8;
+  uint32_t lo = q[0];
+  int acc = 0;
+#pragma unroll
+  for (int k = 0; k < htaps; k += 4) {
+    const uint32_t hi = q[(k >> 2) + 1];
+    const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, sh);  // taps k..k+3 (bytes, LE)
+    lo = hi;
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, __builtin_amdgcn_perm(0u, w, 0x0c010c00u)),
+                                 __builtin_bit_cast(short2_t, hcp[k >> 1]), acc, false);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, __builtin_amdgcn_perm(0u, w, 0x0c030c02u)),
+                                 __builtin_bit_cast(short2_t, hcp[(k >> 1) + 1]), acc, false);
+  }
+  return sws_range(min(acc >> 7, 32767), range);
+}
+
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+
+// HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio)
+template <int HT, int NPV>
 __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
                                                uint8_t *__restrict__ dst, ScaleGeom g,
-                                               const int16_t *__restrict__ hc,
-                                               const int32_t *__restrict__ hp,
-                                               const int16_t *__restrict__ vc,
-                                               const int32_t *__restrict__ vp) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tid = threadIdx.x;
+                                               const int32_t *__restrict__ hcp,   // [dw][htaps/2]
+                                               const int32_t *__restrict__ hp,    // [dw]
+                                               const int32_t *__restrict__ vcp,   // [dh][npv]
+                                               const int32_t *__restrict__ vps) { // [dh] pair start
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * kScaleTileH, f = blockIdx.z;
   const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off;
   uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off;
   const int xe = min(x0 + kScaleTileW, g.dw), ye = min(y0 + kScaleTileH, g.dh);
-  const int r0 = vp[y0], r1 = vp[ye - 1] + g.vtaps;
-  const int c0 = hp[x0], c1 = hp[xe - 1] + g.htaps;
-  const int nr = r1 - r0, nc = c1 - c0;
-  uint8_t *st = smem;
-  int16_t *ht = (int16_t *)(smem + (size_t)g.lds_rows * g.lds_cols);
-
-  for (int i = tid; i < nr * nc; i += 256) {
-    const int r = i / nc, cc = i - r * nc;
-    st[r * g.lds_cols + cc] = s[(size_t)(r0 + r) * g.s_stride + c0 + cc];
-  }
-  __syncthreads();
-  for (int i = tid; i < nr * kScaleTileW; i += 256) {
-    const int r = i >> 6, x = i & 63, xx = x0 + x;
-    if (xx < g.dw) {
-      const int16_t *fc = hc + (size_t)xx * g.htaps;
-      const uint8_t *row = st + r * g.lds_cols + (hp[xx] - c0);
-      int val = 0;
-      for (int j = 0; j < g.htaps; j++) val += (int)row[j] * fc[j];
-      val = min(val >> 7, 32767);
-      ht[r * kScaleTileW + x] = (int16_t)sws_range(val, g.range);
+  const int p0 = vps[y0], p1 = vps[ye - 1] + g.npv;  // row pairs [p0, p1)
+  const int nrows = 2 * (p1 - p0);
+  // source window: dwords [cb, cb + nw) of rows [2 p0, 2 p1) (rows clamped to the plane;
+  // the rows past it only meet zero coefficients), staged with coalesced dword loads
+  const int cb = hp[x0] & ~3;
+  const int nw = ((hp[xe - 1] + g.htaps - cb + 3) >> 2) + 1;  // +1: the funnel shift reads one past
+  uint32_t *win = smem;                                       // [nrows][nw]
+  uint32_t *pairs = smem + g.lds_win_words;                   // [p1 - p0][64]
+  if (nw <= 64 && nrows <= 4 * kScaleMaxRowsPerWave && g.sw >= 4) {
+    // wave per row, lane per dword; all of a wave's loads issued before any is waited on.
+    // A dword crossing the row end is loaded from sw-4 and shifted down (bytes >= sw are
+    // never used).
+    uint32_t v[kScaleMaxRowsPerWave];
+    const int col = cb + 4 * lane, lcol = min(col, g.sw - 4);
+    const uint32_t drop = (uint32_t)(col - lcol) * 8;
+    const uint8_t *sc = s + lcol;
+#pragma unroll
+    for (int j = 0; j < kScaleMaxRowsPerWave; j++)  // unconditional: every address is in-plane
+      v[j] = *(const u32_unaligned *)(sc + (size_t)min(2 * p0 + wave + 4 * j, g.sh - 1) * g.s_stride);
+#pragma unroll
+    for (int j = 0; j < kScaleMaxRowsPerWave; j++) {
+      const int r = wave + 4 * j;
+      if (r < nrows && lane < nw) win[r * nw + lane] = v[j] >> drop;
+    }
+  } else {
+    for (int i = tid; i < nrows * nw; i += 256) {
+      const int r = i / nw, c = i - r * nw;
+      const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
+      const int col = cb + 4 * c;
+      uint32_t v = 0;
+      for (int bb = 0; bb < 4; bb++)
+        if (col + bb < g.sw) v |= (uint32_t)rp[col + bb] << (8 * bb);
+      win[i] = v;
     }
   }
+  const int x = min(x0 + lane, g.dw - 1);  // clamped: tail lanes redo the last column
+  const int32_t *hc = hcp + (size_t)x * (g.htaps >> 1);
+  int32_t hreg[HT ? HT / 2 : 8];  // HT taps (or up to 16 at runtime) in registers
+#pragma unroll
+  for (int k = 0; k < (HT ? HT / 2 : 8); k++) hreg[k] = (2 * k < g.htaps) ? hc[k] : 0;
+  const int off = hp[x] - cb;
   __syncthreads();
-  for (int i = tid; i < kScaleTileH * kScaleTileW; i += 256) {
-    const int y = i >> 6, x = i & 63, yy = y0 + y, xx = x0 + x;
-    if (yy < g.dh && xx < g.dw) {
-      const int16_t *fc = vc + (size_t)yy * g.vtaps;
-      const int16_t *col = ht + (vp[yy] - r0) * kScaleTileW + x;
-      int val = 64 << 12;
-      for (int j = 0; j < g.vtaps; j++) val += (int)col[j * kScaleTileW] * fc[j];
-      val >>= 19;
-      d[(size_t)yy * g.d_stride + xx] = (uint8_t)min(max(val, 0), 255);
+  for (int p = wave; p < p1 - p0; p += 4) {
+    int a, b;
+    if (HT || g.htaps <= 16) {
+      a = hscale_lds<HT>(win + (2 * p) * nw, off, hreg, g.htaps, g.range);
+      b = hscale_lds<HT>(win + (2 * p + 1) * nw, off, hreg, g.htaps, g.range);
+    } else {
+      a = hscale_lds<0>(win + (2 * p) * nw, off, hc, g.htaps, g.range);
+      b = hscale_lds<0>(win + (2 * p + 1) * nw, off, hc, g.htaps, g.range);
     }
+    pairs[p * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
+  }
+  __syncthreads();
+  if (x0 + lane >= g.dw) return;
+  for (int y = y0 + wave; y < ye; y += 4) {
+    const int32_t *vc = vcp + (size_t)y * g.npv;
+    const uint32_t *col = pairs + (vps[y] - p0) * 64 + lane;
+    int acc = 64 << 12;
+    const int npv = NPV ? NPV : g.npv;
+#pragma unroll
+    for (int k = 0; k < npv; k++)
+      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, col[k * 64]),
+                                   __builtin_bit_cast(short2_t, vc[k]), acc, false);
+    d[(size_t)y * g.d_stride + x0 + lane] = (uint8_t)min(max(acc >> 19, 0), 255);
   }
 }
 
