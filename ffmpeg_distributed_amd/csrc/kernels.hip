@@ -24,6 +24,12 @@
 #ifndef MJG_ENC_WAVES_PER_EU
 #define MJG_ENC_WAVES_PER_EU 3  // k_encode occupancy target (waves per SIMD); measured best (v8)
 #endif
+#ifndef MJG_TEMPORAL_LOADS
+#define MJG_TEMPORAL_LOADS 0  // 1: plain (L2-retained) pixel row loads instead of nontemporal
+#endif
+#ifndef MJG_RC_LUT
+#define MJG_RC_LUT 1  // tv->pc range conversion through a 512-byte LDS table (0: fp32 fma + med3)
+#endif
 #ifndef MJG_ABLATE
 #define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store
 #endif
@@ -321,7 +327,11 @@ __device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s) {
   if (fast) {
 #pragma unroll
     for (int r = 0; r < 8; r++)
+#if MJG_TEMPORAL_LOADS
+      raw[r] = *(const uint64_t *)(base + (size_t)r * s.stride);
+#else
       raw[r] = __builtin_nontemporal_load((const uint64_t *)(base + (size_t)r * s.stride));
+#endif
   }
   return fast;
 }
@@ -431,6 +441,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) int s_m2[72];       // pass-2 dot rows + per-row constant
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
+  __shared__ uint8_t s_rc[MJG_RC_LUT ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   // per wave: the current frame's histogram (kCount) or code tables (kEmitFrame)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
@@ -446,6 +457,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_scat[tid] = kScreenScatter[tid];
   }
   if (tid < 8) s_m2[64 + tid] = kPass2Add[tid];
+  if (MJG_RC_LUT && RC)
+    for (int i = tid; i < 512; i += 64 * kWavesPerWg)
+      s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
   uint32_t *s_pk = s_pk_all[wave];
   uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
   if (MODE == kCount)
@@ -524,7 +538,20 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       p[6] = (float)((hi >> 16) & 255u);  // v_cvt_f32_ubyte2
       p[7] = (float)((hi >> 24) & 255u);  // v_cvt_f32_ubyte3
       float t0, t1, t2, t3;
-      if (rc) {
+      if (rc && MJG_RC_LUT) {
+        // LDS address (tab << 8) | pixel in one v_perm, the table byte OR'ed into kM's
+        // mantissa: kM + range(p) exactly as the fp32 path below produces it
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+          const uint32_t a = __builtin_amdgcn_perm((uint32_t)tab, x < 4 ? lo : hi,
+                                                   0x0c0c0400u | (uint32_t)(x & 3));
+          p[x] = __uint_as_float(0x4B400000u | (uint32_t)s_rc[a]);
+        }
+        t0 = (p[0] - 2.0f * kM) + p[7];
+        t1 = (p[1] - 2.0f * kM) + p[6];
+        t2 = (p[2] - 2.0f * kM) + p[5];
+        t3 = (p[3] - 2.0f * kM) + p[4];
+      } else if (rc) {
 #pragma unroll
         for (int x = 0; x < 8; x++)
           p[x] = __builtin_amdgcn_fmed3f(__builtin_fmaf(p[x], rA, rB) + kM, kM, kM + 255.0f);

@@ -85,7 +85,9 @@ void mjg_close(mjg_ctx *ctx);
 
 /* Bytes of one packed I420 input frame (src_w x src_h). */
 size_t mjg_frame_bytes(const mjg_ctx *ctx);
-/* The constant per-config JPEG header (SOI .. SOS) every frame starts with. */
+/* The per-config JPEG header (SOI .. SOS) every frame starts with.  With
+ * MJG_F_HUFFMAN_OPTIMAL each frame carries its own DHT; this returns the header with the
+ * default tables (same layout, different DHT contents). */
 int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 
 /* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously on the ctx

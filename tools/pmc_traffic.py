@@ -14,8 +14,12 @@ out, calib_bytes = sys.argv[1], int(sys.argv[2])
 cal = load([os.path.join(out, "calib")])
 cal_fetch = sum(v["FETCH_SIZE"] for v in cal.values())  # one kernel
 per_unit = calib_bytes / cal_fetch
-fetch = load([os.path.join(out, "fetch")])["mjg::k_encode"]["FETCH_SIZE"]
-write = load([os.path.join(out, "write")])["mjg::k_encode"]["WRITE_SIZE"]
+def _enc(d):  # the k_encode instantiation (template arguments in the name)
+    return next(v for k, v in d.items() if "k_encode" in k)
+
+
+fetch = _enc(load([os.path.join(out, "fetch")]))["FETCH_SIZE"]
+write = _enc(load([os.path.join(out, "write")]))["WRITE_SIZE"]
 frames, W, H = 120, 3840, 2160
 res = {
     "kernel": "mjg::k_encode",
