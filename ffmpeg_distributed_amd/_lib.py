@@ -25,6 +25,10 @@ MJG_F_DEBUG_COEFS = 2
 MJG_F_SWS_NO_BITEXACT = 4
 MJG_F_COM_ITU601 = 8
 MJG_F_HUFFMAN_OPTIMAL = 16
+MJG_F_RST = 32
+
+# mjg_config.chroma_format
+CHROMA_FORMATS = {"420": 0, "422": 1, "444": 2}
 
 KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write", "huff")
 MJG_NUM_KERNELS = len(KERNEL_NAMES)
@@ -52,6 +56,7 @@ class MjgConfig(C.Structure):
         ("in_full_range", C.c_int32), ("qscale", C.c_int32),
         ("sar_num", C.c_int32), ("sar_den", C.c_int32),
         ("max_batch", C.c_int32), ("flags", C.c_uint32),
+        ("chroma_format", C.c_int32),
     ]
 
 
@@ -111,11 +116,13 @@ def device_count() -> int:
     return check(load().mjg_device_count())
 
 
-def build_header(dst_w: int, dst_h: int, qscale: int, sar=(1, 1), com_itu601: bool = False) -> bytes:
+def build_header(dst_w: int, dst_h: int, qscale: int, sar=(1, 1), com_itu601: bool = False,
+                 chroma: str = "420", rst: bool = False) -> bytes:
     """The per-config JPEG header, computed on the host (no GPU needed)."""
     L = load()
-    cfg = MjgConfig(dst_w, dst_h, dst_w, dst_h, 1, qscale, sar[0], sar[1], 1,
-                    MJG_F_COM_ITU601 if com_itu601 else 0)
+    flags = (MJG_F_COM_ITU601 if com_itu601 else 0) | (MJG_F_RST if rst else 0)
+    cfg = MjgConfig(dst_w, dst_h, dst_w, dst_h, 1, qscale, sar[0], sar[1], 1, flags,
+                    CHROMA_FORMATS[str(chroma)])
     n = C.c_size_t()
     check(L.mjg_build_header(C.byref(cfg), None, 0, C.byref(n)))
     buf = (C.c_uint8 * n.value)()

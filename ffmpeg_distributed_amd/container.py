@@ -3,9 +3,10 @@ in-process).  The reference's worker reads a Matroska segment on stdin and write
 Matroska segment on stdout (ffmpeg_distributed.py:133-135); its output must stay
 readable by the ffmpeg concat demuxer the reference runs at :216-227.
 
-  Y4MReader   YUV4MPEG2 raw 4:2:0 frames (what `ffmpeg -f yuv4mpegpipe` emits)
-  MkvReader   Matroska with V_UNCOMPRESSED I420 video (a `-c copy` split of raw video)
-              or V_MJPEG (used by the tests to read our own output back)
+  Y4MReader   YUV4MPEG2 raw 4:2:0 / 4:2:2 / 4:4:4 frames (what `ffmpeg -f yuv4mpegpipe` emits)
+  y4m_header  the matching writer's stream header
+  MkvReader   Matroska with V_UNCOMPRESSED I420 / Y42B / 444P video (a `-c copy` split of
+              raw video) or V_MJPEG (used by the tests to read our own output back)
   MkvWriter   Matroska with one V_MJPEG video track, one keyframe SimpleBlock per frame
 """
 from __future__ import annotations
@@ -93,11 +94,35 @@ class StreamInfo:
     full_range: bool = False
     codec: str = "rawvideo"
     frame_bytes: int = 0
+    chroma: str = "420"                 # planar sampling: "420", "422", "444"
 
     def __post_init__(self):
         if not self.frame_bytes:
-            cw, ch = (self.width + 1) // 2, (self.height + 1) // 2
+            hs, vs = {"420": (1, 1), "422": (1, 0), "444": (0, 0)}[self.chroma]
+            cw, ch = (self.width + hs) >> hs, (self.height + vs) >> vs
             self.frame_bytes = self.width * self.height + 2 * cw * ch
+
+
+# Matroska V_UNCOMPRESSED ColourSpace fourccs (libavformat/raw.c ff_raw_pix_fmt_tags)
+MKV_FOURCC_CHROMA = {b"I420": "420", b"": "420", b"Y42B": "422", b"444P": "444"}
+
+
+def y4m_chroma(tag: str) -> str:
+    """Sampling of a YUV4MPEG2 'C' tag (yuv4mpegdec.c: 420jpeg/420paldv/420mpeg2/420, 422, 444)."""
+    for c in ("420", "422", "444"):
+        if tag == c or (c == "420" and tag in ("420jpeg", "420paldv", "420mpeg2")):
+            return c
+    raise ValueError(f"y4m colorspace C{tag}: only 8-bit 4:2:0 / 4:2:2 / 4:4:4")
+
+
+def y4m_header(info: "StreamInfo") -> bytes:
+    """YUV4MPEG2 stream header for `info` (yuv4mpegenc.c field order)."""
+    c = {"420": "420jpeg", "422": "422", "444": "444"}[info.chroma]
+    a = f"A{info.sar[0]}:{info.sar[1]}" if info.sar != (0, 0) else "A0:0"
+    x = " XCOLORRANGE=FULL" if info.full_range else ""
+    fps = info.fps
+    return (f"YUV4MPEG2 W{info.width} H{info.height} F{fps.numerator}:{fps.denominator} Ip {a} "
+            f"C{c}{x}\n").encode()
 
 
 class Y4MReader:
@@ -109,7 +134,7 @@ class Y4MReader:
         if not line.startswith(b"YUV4MPEG2"):
             raise ValueError("not a YUV4MPEG2 stream")
         w = h = None
-        fps, sar, full = Fraction(25), (0, 0), False
+        fps, sar, full, chroma = Fraction(25), (0, 0), False, "420"
         for tok in line.split()[1:]:
             t, v = tok[:1], tok[1:].decode()
             if t == b"W":
@@ -123,13 +148,12 @@ class Y4MReader:
                 n, d = v.split(":")
                 sar = (int(n), int(d))
             elif t == b"C":
-                if not v.startswith("420"):
-                    raise ValueError(f"y4m colorspace C{v}: only 4:2:0 8-bit")
+                chroma = y4m_chroma(v)
             elif t == b"X" and v.upper().startswith("COLORRANGE="):
                 full = v.split("=", 1)[1].upper() == "FULL"
         if not w or not h:
             raise ValueError("y4m header without W/H")
-        self.info = StreamInfo(w, h, fps, sar, full)
+        self.info = StreamInfo(w, h, fps, sar, full, chroma=chroma)
 
     def _readline(self) -> bytes:
         out = bytearray()
@@ -272,8 +296,9 @@ class MkvReader:
         if tr.display != (0, 0) and tr.width and tr.height:
             s = Fraction(tr.display[0] * tr.height, tr.display[1] * tr.width)
             sar = (s.numerator, s.denominator)
+        chroma = MKV_FOURCC_CHROMA.get(tr.colour_space, "420") if tr.codec == "V_UNCOMPRESSED" else "420"
         return StreamInfo(tr.width, tr.height, fps.limit_denominator(1001), sar,
-                          full_range=tr.colour_range == 2, codec=tr.codec)
+                          full_range=tr.colour_range == 2, codec=tr.codec, chroma=chroma)
 
     def duration_seconds(self) -> Optional[float]:
         return None if self.duration is None else self.duration * self.timescale / 1e9

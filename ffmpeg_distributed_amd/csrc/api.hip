@@ -37,16 +37,32 @@ int set_err(int code, const char *fmt, ...) {
   } while (0)
 
 // JPEG header of the profile: mjpegenc_common.c ff_mjpeg_encode_picture_header for
-// AV_CODEC_ID_MJPEG 4:2:0, -bitexact (no COM), equal luma/chroma matrices (one DQT),
-// frame threading (no DRI), -huffman default (one DHT with DC0, DC1, AC0, AC1).
+// AV_CODEC_ID_MJPEG, -bitexact (no COM), equal luma/chroma matrices (one DQT), DRI only
+// with slice threading (RST mode), -huffman default (one DHT with DC0, DC1, AC0, AC1);
+// SOF0 sampling factors from ff_mjpeg_init_hvsample.
 struct ByteWriter {
   std::vector<uint8_t> b;
   void u8(int v) { b.push_back((uint8_t)v); }
   void u16(int v) { u8(v >> 8); u8(v); }
 };
 
+// (h, v) sampling factors of Y, Cb, Cr (ff_mjpeg_init_hvsample; 4:4:4 is all 1x2).
+void hvsample(int cfmt, int hs[3], int vs[3]) {
+  if (cfmt == MJG_CHROMA_444) {
+    hs[0] = hs[1] = hs[2] = 1;
+    vs[0] = vs[1] = vs[2] = 2;
+    return;
+  }
+  hs[0] = vs[0] = 2;
+  hs[1] = hs[2] = 1;
+  vs[1] = vs[2] = cfmt == MJG_CHROMA_422 ? 2 : 1;
+}
+
 std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sar_num, int sar_den,
-                                  bool com_itu601, size_t *dht_pos = nullptr, size_t *dht_end = nullptr) {
+                                  bool com_itu601, int cfmt, bool rst, size_t *dht_pos = nullptr,
+                                  size_t *dht_end = nullptr) {
+  int hs[3], vs[3];
+  hvsample(cfmt, hs, vs);
   ByteWriter o;
   o.u16(0xFFD8);
   if (sar_num > 0 && sar_den > 0) {
@@ -69,6 +85,11 @@ std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sa
   o.u16(2 + 65);
   o.u8(0x00);
   for (int i = 0; i < 64; i++) o.u8(mprime[kZigzag[i]]);
+  if (rst) {  // jpeg_table_header: DRI, interval = MCUs per MCU row
+    o.u16(0xFFDD);
+    o.u16(4);
+    o.u16((w - 1) / (8 * hs[0]) + 1);
+  }
   if (dht_pos) *dht_pos = o.b.size();
   o.u16(0xFFC4);
   const size_t len_at = o.b.size();
@@ -96,9 +117,11 @@ std::vector<uint8_t> build_header(int w, int h, const uint8_t mprime[64], int sa
   o.u16(h);
   o.u16(w);
   o.u8(3);
-  o.u8(1); o.u8(0x22); o.u8(0);
-  o.u8(2); o.u8(0x11); o.u8(0);
-  o.u8(3); o.u8(0x11); o.u8(0);
+  for (int c = 0; c < 3; c++) {
+    o.u8(c + 1);
+    o.u8((hs[c] << 4) | vs[c]);
+    o.u8(0);
+  }
   o.u16(0xFFDA);
   o.u16(12);
   o.u8(3);
@@ -150,6 +173,10 @@ struct mjg_ctx {
   uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
   uint32_t *d_frame_bits = nullptr, *d_status = nullptr, *d_work = nullptr;
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
+  // RST mode: per-segment stuffed sizes and their offsets after the frame header
+  bool rst = false;
+  uint64_t *d_seg_size = nullptr;
+  uint32_t *d_seg_off = nullptr;
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
   // -huffman optimal
@@ -181,7 +208,7 @@ void free_ctx(mjg_ctx *c) {
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
                   c->d_chunk_off, c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
                   c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->d_hist, c->d_ftabs,
-                  c->d_dht_nval, c->d_hdr_lens, c->d_dht, c->ps[0].hcp,
+                  c->d_dht_nval, c->d_hdr_lens, c->d_dht, c->d_seg_size, c->d_seg_off, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
                   c->ps[1].vps};
   for (void *p : ptrs)
@@ -197,11 +224,13 @@ void free_ctx(mjg_ctx *c) {
   delete c;
 }
 
+// chroma: plane subsampling shifts (hsub, vsub) select the siting get_local_pos(shift, -513)
 int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh, int chroma,
-                      bool bitexact) {
-  const int pos = chroma ? sws_local_pos(1, -513) : sws_local_pos(0, 0);
-  if (!make_sws_filter(sw, dw, 1 << 14, 4, bitexact, pos, pos, &p.hf) ||
-      !make_sws_filter(sh, dh, 1 << 12, 2, bitexact, pos, pos, &p.vf))
+                      int hsub, int vsub, bool bitexact) {
+  const int hpos = chroma ? sws_local_pos(hsub, -513) : sws_local_pos(0, 0);
+  const int vpos = chroma ? sws_local_pos(vsub, -513) : sws_local_pos(0, 0);
+  if (!make_sws_filter(sw, dw, 1 << 14, 4, bitexact, hpos, hpos, &p.hf) ||
+      !make_sws_filter(sh, dh, 1 << 12, 2, bitexact, vpos, vpos, &p.vf))
     return set_err(MJG_E_INVALID, "scale %dx%d -> %dx%d needs swscale's cascade (unsupported)", sw,
                    sh, dw, dh);
   for (int i = 1; i < dw; i++)
@@ -273,6 +302,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     return set_err(MJG_E_INVALID, "max_batch %d not in 1..65535", k.max_batch);
   if (k.sar_num < 0 || k.sar_den < 0 || k.sar_num > 65535 || k.sar_den > 65535)
     return set_err(MJG_E_INVALID, "bad SAR %d:%d", k.sar_num, k.sar_den);
+  if (k.chroma_format < MJG_CHROMA_420 || k.chroma_format > MJG_CHROMA_444)
+    return set_err(MJG_E_INVALID, "chroma_format %d", k.chroma_format);
+  if ((k.flags & MJG_F_RST) && (k.flags & MJG_F_HUFFMAN_OPTIMAL))
+    return set_err(MJG_E_INVALID, "RST (slice threading) forces -huffman default");
 
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -281,8 +314,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
 
   c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
-  const int scw = (k.src_w + 1) >> 1, sch = (k.src_h + 1) >> 1;
-  const int w = k.dst_w, h = k.dst_h, cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+  const int cf = k.chroma_format;
+  const int hsh = cf == MJG_CHROMA_444 ? 0 : 1, vsh = cf == MJG_CHROMA_420 ? 1 : 0;
+  const int scw = (k.src_w + hsh) >> hsh, sch = (k.src_h + vsh) >> vsh;
+  const int w = k.dst_w, h = k.dst_h, cw = (w + hsh) >> hsh, ch = (h + vsh) >> vsh;
   c->in_frame_bytes = (size_t)k.src_w * k.src_h + 2 * (size_t)scw * sch;
   c->enc_frame_bytes = (size_t)w * h + 2 * (size_t)cw * ch;
 
@@ -291,9 +326,19 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   g.h = h;
   g.cw = cw;
   g.ch = ch;
-  g.mbw = (w + 15) / 16;
-  g.nmcu = g.mbw * ((h + 15) / 16);
-  g.nchunks = (g.nmcu * 6 + 63) / 64;  // chunks of 64 blocks (one wave each)
+  g.bpm = cf == MJG_CHROMA_422 ? 8 : 6;
+  g.bpm_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.bpm - 1) / (uint64_t)g.bpm);
+  g.lmw = cf == MJG_CHROMA_444 ? 8 : 16;
+  g.cmh = cf == MJG_CHROMA_420 ? 8 : 16;
+  g.mbw = (w + g.lmw - 1) / g.lmw;
+  const int mbh = (h + 15) / 16;
+  g.nmcu = g.mbw * mbh;
+  // RST: one segment per MCU row (mpegvideo clips the slice count to mb_height, so a
+  // single-row picture has no restart markers)
+  c->rst = (k.flags & MJG_F_RST) && mbh > 1;
+  g.nseg = c->rst ? mbh : 1;
+  g.seg_blocks = (c->rst ? g.mbw : g.nmcu) * g.bpm;
+  g.nchunks = (g.seg_blocks + 63) / 64;  // chunks of 64 blocks (one wave each) per segment
   g.y_stride = w;
   g.c_stride = cw;
   g.u_off = (long long)w * h;
@@ -309,8 +354,8 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     c->mprime[i] = (uint8_t)v;
     c->qmat[i] = (int32_t)((2ull << 21) / (uint64_t)(16 * v));
   }
-  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0,
-                        &c->dht_pos, &c->dht_end);
+  c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
+                        c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
@@ -336,18 +381,35 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     const float b2 = (float)(B * B);
     memcpy(&tabs[608 + (i & 7) * 8 + ro], &b2, 4);
   }
+  // [672, 680): block-of-MCU descriptors in coding order (EncGeom): plane | chroma table << 2 |
+  // dx8 << 3 | dy8 << 4 | DC predecessor distance << 8 (ff_mjpeg_encode_mb order; the
+  // predecessor is the previous block of the same component)
+  {
+    static const uint8_t kPlane[3][8] = {{0, 0, 0, 0, 1, 2}, {0, 0, 0, 0, 1, 1, 2, 2}, {0, 0, 1, 1, 2, 2}};
+    static const uint8_t kDx[3][8] = {{0, 1, 0, 1, 0, 0}, {0, 1, 0, 1, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};
+    static const uint8_t kDy[3][8] = {{0, 0, 1, 1, 0, 0}, {0, 0, 1, 1, 0, 1, 0, 1}, {0, 1, 0, 1, 0, 1}};
+    for (int j = 0; j < g.bpm; j++) {
+      const int pl = kPlane[cf][j];
+      int delta = 0;  // distance back to the previous block of plane pl (wrapping to the previous MCU)
+      for (int d = 1; d <= g.bpm && !delta; d++)
+        if (kPlane[cf][((j - d) % g.bpm + g.bpm) % g.bpm] == pl) delta = d;
+      tabs[672 + j] = (uint32_t)pl | (pl ? 4u : 0u) | ((uint32_t)kDx[cf][j] << 3) |
+                      ((uint32_t)kDy[cf][j] << 4) | ((uint32_t)delta << 8);
+    }
+  }
 
-  const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks;
+  const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
   int rc;
   if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
       (rc = dmalloc(&c->d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
       (rc = dmalloc(&c->d_group_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
-      (rc = dmalloc(&c->d_frame_bits, B)) || (rc = dmalloc(&c->d_status, 4)) ||
+      (rc = dmalloc(&c->d_frame_bits, B * NS)) || (rc = dmalloc(&c->d_status, 4)) ||
       (rc = dmalloc(&c->d_work, 1)) ||
       (rc = dmalloc(&c->d_frame_size, B)) || (rc = dmalloc(&c->d_frame_offsets, B + 1)))
     return rc;
-  c->out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096);
+  if (c->rst && ((rc = dmalloc(&c->d_seg_size, B * NS)) || (rc = dmalloc(&c->d_seg_off, B * NS)))) return rc;
+  c->out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096 + 2 * NS);
   if ((rc = dmalloc(&c->d_out, c->out_cap))) return rc;
   if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
   if (c->optimal &&
@@ -355,7 +417,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
        (rc = dmalloc(&c->d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&c->d_dht_nval, B * 4)) ||
        (rc = dmalloc(&c->d_hdr_lens, B))))
     return rc;
-  if (g.debug_coefs && (rc = dmalloc(&c->d_dbg, B * (size_t)g.nmcu * 6 * 64))) return rc;
+  if (g.debug_coefs && (rc = dmalloc(&c->d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
 #ifdef MJG_STAMPS
   if (!c->d_dbg && (rc = dmalloc(&c->d_dbg, (size_t)1 << 22))) return rc;  // 512K stamps
 #endif
@@ -367,8 +429,8 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
 
   if (c->scale) {
     const bool bitexact = !(k.flags & MJG_F_SWS_NO_BITEXACT);
-    if ((rc = setup_plane_scale(c, c->ps[0], k.src_w, k.src_h, w, h, 0, bitexact)) ||
-        (rc = setup_plane_scale(c, c->ps[1], scw, sch, cw, ch, 1, bitexact)))
+    if ((rc = setup_plane_scale(c, c->ps[0], k.src_w, k.src_h, w, h, 0, 0, 0, bitexact)) ||
+        (rc = setup_plane_scale(c, c->ps[1], scw, sch, cw, ch, 1, hsh, vsh, bitexact)))
       return rc;
     for (int p = 0; p < 2; p++) {
       ScaleGeom &sg = c->ps[p].g;
@@ -405,17 +467,18 @@ void tmark(mjg_ctx *c, int k, int end) {
 
 int launch_write(mjg_ctx *c, int n) {
   const EncGeom &g = c->geom;
-  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n;
+  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n * g.nseg;
   HIP_TRY(hipMemsetAsync(c->d_status, 0, 4, c->stream));
   tmark(c, MJG_K_WRITE, 0);
   k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
                                        (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status,
                                        c->optimal ? c->d_hdr_lens : nullptr, (int)c->dht_pos,
-                                       (int)c->dht_end, c->d_dht, c->d_dht_nval);
+                                       (int)c->dht_end, c->d_dht, c->d_dht_nval, c->d_seg_off,
+                                       c->d_seg_size, g.nseg);
   k_write<<<(ngroups + 3) / 4, 256, 0, c->stream>>>(
       c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
       c->d_frame_offsets, (int)c->hdr.size(), c->optimal ? c->d_hdr_lens : nullptr, g.nchunks, gpf,
-      ngroups, c->d_out, (uint64_t)c->out_cap);
+      ngroups, c->d_out, (uint64_t)c->out_cap, c->d_seg_off, g.nseg);
   tmark(c, MJG_K_WRITE, 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->h_sizes, c->d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -523,7 +586,8 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     HIP_TRY(hipGetLastError());
     enc_in = c->d_scaled;
   }
-  const int ntasks = g.nchunks * n;
+  const int ntasks = g.nchunks * g.nseg * n;
+  const int nsegs = g.nseg * n;  // entropy-coded segments of this submit
   const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
   if (c->optimal) {  // pass 1: symbol counts per frame, then the frame's tables
     tmark(c, MJG_K_HUFF, 0);
@@ -542,22 +606,29 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_BITS, 0);
-  k_scan_bits<<<n, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, g.nchunks,
-                                         c->d_work);
+  k_scan_bits<<<nsegs, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits,
+                                             g.nchunks, c->d_work);
   tmark(c, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_COUNT_FF, 0);
   const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
-  k_count_ff<<<(gpf * n + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits, c->d_chunk_off,
-                                                       c->d_frame_bits, c->d_group_ff, g.nchunks,
-                                                       gpf, gpf * n);
+  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits, c->d_chunk_off,
+                                                           c->d_frame_bits, c->d_group_ff, g.nchunks,
+                                                           gpf, gpf * nsegs);
   tmark(c, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_FF, 0);
   // optimal: header = default header - its 348 table values + the frame's
-  k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
-                                       gpf, (int)c->hdr.size(), c->optimal ? c->d_dht_nval : nullptr,
-                                       (int)c->hdr.size() - 348, c->d_hdr_lens);
+  if (c->rst) {  // segment sizes (each with its RSTn / EOI trailer), then per-frame offsets
+    k_scan_ff<<<nsegs, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_seg_size,
+                                             gpf, 0, nullptr, 0, nullptr);
+    k_seg_sizes<<<n, 64, 0, c->stream>>>(c->d_seg_size, g.nseg, (int)c->hdr.size(), c->d_seg_off,
+                                         c->d_frame_size);
+  } else {
+    k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
+                                         gpf, (int)c->hdr.size(), c->optimal ? c->d_dht_nval : nullptr,
+                                         (int)c->hdr.size() - 348, c->d_hdr_lens);
+  }
   tmark(c, MJG_K_SCAN_FF, 1);
   HIP_TRY(hipGetLastError());
   int rc = launch_write(c, n);
@@ -656,8 +727,9 @@ int mjg_kernel_times(mjg_ctx *c, double *ms, int *launches, int reset) {
 int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *len) {
   if (!cfg) return set_err(MJG_E_INVALID, "null cfg");
   if (cfg->dst_w < 1 || cfg->dst_h < 1 || cfg->dst_w > 65535 || cfg->dst_h > 65535 ||
-      cfg->qscale < 1 || cfg->qscale > 31)
-    return set_err(MJG_E_INVALID, "bad size / qscale");
+      cfg->qscale < 1 || cfg->qscale > 31 || cfg->chroma_format < MJG_CHROMA_420 ||
+      cfg->chroma_format > MJG_CHROMA_444)
+    return set_err(MJG_E_INVALID, "bad size / qscale / chroma_format");
   if (cfg->sar_num < 0 || cfg->sar_den < 0 || cfg->sar_num > 65535 || cfg->sar_den > 65535)
     return set_err(MJG_E_INVALID, "bad SAR %d:%d", cfg->sar_num, cfg->sar_den);
   uint8_t mp[64];
@@ -665,8 +737,9 @@ int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *le
     const int v = i == 0 ? 8 : ((kMpeg1Intra[i] * cfg->qscale) >> 3);
     mp[i] = (uint8_t)(v > 255 ? 255 : v);
   }
+  const bool rst = (cfg->flags & MJG_F_RST) && (cfg->dst_h + 15) / 16 > 1;
   const std::vector<uint8_t> h = build_header(cfg->dst_w, cfg->dst_h, mp, cfg->sar_num, cfg->sar_den,
-                                             (cfg->flags & MJG_F_COM_ITU601) != 0);
+                                             (cfg->flags & MJG_F_COM_ITU601) != 0, cfg->chroma_format, rst);
   if (len) *len = h.size();
   if (!out) return MJG_OK;
   if (cap < h.size()) return set_err(MJG_E_CAPACITY, "header needs %zu bytes", h.size());
@@ -692,7 +765,7 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   if (!c->d_dbg) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
   int rc = mjg_sync(c, nullptr, nullptr);
   if (rc) return rc;
-  const size_t nb = (size_t)c->geom.nmcu * 6;  // dbg buffer: frame-major, block order
+  const size_t nb = (size_t)c->geom.nmcu * c->geom.bpm;  // dbg buffer: frame-major, coding order
   if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
   // the kernel stores each quantised block in natural (raster) order

@@ -42,7 +42,7 @@ constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 bl
 // fp32 exact-integer arithmetic (k_encode): adding kM = 1.5*2^23 rounds to an integer
 // (round-to-nearest-even) and keeps it in the low mantissa bits; kMb = kM + 32768 leaves
 // value + 32768 in the low 16 bits.  kRnd = 2^-10 turns floor(x/512 + 1/2) into RNE.
-constexpr int kTabWords = 672;  // device table block, see open_ctx
+constexpr int kTabWords = 680;  // device table block, see open_ctx
 constexpr float kM = 12582912.0f;
 constexpr float kMb = 12615680.0f;
 constexpr float kRnd = 0x1p-10f;
@@ -71,15 +71,33 @@ __device__ static constexpr uint8_t kScreenScatter[64] = {
 __device__ static constexpr int kPass2Add[8] = {8 - 8 * 32768, 1 << 16, 1 << 16, 1 << 16,
                                                 8, 1 << 16, 1 << 16, 1 << 16};
 
+// Frame geometry.  A frame is a raster of MCUs of `bpm` blocks each (4:2:0: 16x16, Y0-3 Cb
+// Cr; 4:2:2: 16x16, Y0-3 Cb0 Cb1 Cr0 Cr1; 4:4:4: 8x16, Y0 Y1 Cb0 Cb1 Cr0 Cr1 -- FFmpeg's
+// coding order, see oracle/mjpeg_oracle.c or_layouts), split into `nseg` entropy-coded
+// segments per frame (1, or one per MCU row in RST mode) of seg_blocks blocks, each cut into
+// `nchunks` chunks of 64 blocks.  The per-block-of-MCU descriptors (plane, table, 8x8 offset
+// in the MCU, DC predecessor distance) are words [672, 680) of the table block.
 struct EncGeom {
   int w, h;            // encoded size
   int cw, ch;          // chroma plane size
-  int mbw, nmcu, nchunks;
+  int mbw, nmcu;       // MCUs per row, per frame
+  int bpm;             // blocks per MCU (6 or 8)
+  uint32_t bpm_magic;  // ceil(2^32 / bpm): b / bpm == umulhi(b, bpm_magic) for b < 2^29
+  int lmw, cmh;        // luma MCU width (16, 4:4:4: 8), chroma MCU height (8, 4:2:2/4:4:4: 16)
+  int nseg, seg_blocks, nchunks;  // segments per frame, blocks / chunks per segment
   int y_stride, c_stride;
   long long frame_stride, u_off, v_off;
   int range_convert;   // 1: yuv420p (tv) input without scale -> swscale tv->pc per pixel
   int debug_coefs;
 };
+
+// block descriptor word: bits 0-1 plane, 2 Huffman table (chroma), 3 dx (8 px), 4 dy (8 px),
+// 8-11 distance to the previous block of the same component in coding order
+__device__ __forceinline__ int desc_tab(uint32_t d) { return (int)((d >> 2) & 1u); }
+__device__ __forceinline__ int desc_delta(uint32_t d) { return (int)(d >> 8); }
+__device__ __forceinline__ int block_in_mcu(const EncGeom &g, int b) {
+  return b - g.bpm * (int)__umulhi((uint32_t)b, g.bpm_magic);
+}
 
 
 // ---------------------------------------------------------------- helpers
@@ -360,27 +378,39 @@ __device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s
 // prefetches the next chunk's pixel rows into registers while encoding the current one.
 constexpr int kWavesPerWg = 4;
 
-__device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g, int frame, int b) {
+// Source rectangle of block b (index in the frame's coding order) of `frame`.
+__device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g, int frame, int b,
+                                         const uint32_t *desc) {
   const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
-  const int m = b / 6, blk = b - 6 * (b / 6);
+  const int m = (int)__umulhi((uint32_t)b, g.bpm_magic);
+  const uint32_t d = desc[b - m * g.bpm];
   const int mx = m % g.mbw, my = m / g.mbw;
+  const int plane = (int)(d & 3u), dx = (int)((d >> 3) & 1u) * 8, dy = (int)((d >> 4) & 1u) * 8;
   Src s;
-  if (blk < 4) {
+  if (plane == 0) {
     s.plane = fr;
     s.stride = g.y_stride;
     s.pw = g.w;
     s.ph = g.h;
-    s.x0 = mx * 16 + (blk & 1) * 8;
-    s.y0 = my * 16 + (blk >> 1) * 8;
+    s.x0 = mx * g.lmw + dx;
+    s.y0 = my * 16 + dy;
   } else {
-    s.plane = fr + (blk == 4 ? g.u_off : g.v_off);
+    s.plane = fr + (plane == 1 ? g.u_off : g.v_off);
     s.stride = g.c_stride;
     s.pw = g.cw;
     s.ph = g.ch;
-    s.x0 = mx * 8;
-    s.y0 = my * 8;
+    s.x0 = mx * 8 + dx;
+    s.y0 = my * g.cmh + dy;
   }
   return s;
+}
+
+// Task t (one chunk) -> frame, chunk index in its segment, first block of the segment.
+__device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, int &chunk, int &bbase) {
+  const int seg = t / g.nchunks;
+  chunk = t - seg * g.nchunks;
+  frame = seg / g.nseg;
+  bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
 #ifndef MJG_ENC_BATCH
@@ -389,14 +419,14 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
 constexpr int kBatch = MJG_ENC_BATCH;  // chunks per work unit pulled from the counter
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
-// quantised DCs of the 6 blocks before it (the only possible predecessors), lane 58+i
-// holding block chunk*64-6+i.  Quantised DC = (pixel sum + 32) >> 6 exactly.
-// carry_row: lanes 0..47 load row (lane & 7) of block (lane >> 3) of those 6 blocks
+// quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
+// lane 56+i holding block chunk*64-8+i of the segment.  Quantised DC = (pixel sum + 32) >> 6
+// exactly.  carry_row: lane loads row (lane & 7) of block (lane >> 3) of those 8 blocks
 // (issued early so the load overlaps a chunk's work); carry_finish reduces them.
 __device__ __forceinline__ uint64_t carry_row(const uint8_t *frames, const EncGeom &g, int frame,
-                                              int chunk, int lane) {
-  if (chunk == 0 || lane >= 48) return 0;
-  const Src s = block_src(frames, g, frame, chunk * 64 - 6 + (lane >> 3));
+                                              int bbase, int chunk, int lane, const uint32_t *desc) {
+  if (chunk == 0) return 0;
+  const Src s = block_src(frames, g, frame, bbase + chunk * 64 - 8 + (lane >> 3), desc);
   const uint8_t *row = s.plane + (size_t)min(s.y0 + (lane & 7), s.ph - 1) * s.stride;
   if (s.x0 + 8 <= s.pw && (((uintptr_t)(row + s.x0)) & 7) == 0)
     return *(const uint64_t *)(row + s.x0);
@@ -405,10 +435,10 @@ __device__ __forceinline__ uint64_t carry_row(const uint8_t *frames, const EncGe
   return w;
 }
 
-__device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, bool rc) {
+__device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, bool rc, const EncGeom &g,
+                                            const uint32_t *desc) {
   if (chunk == 0) return 128;
-  const int pb = chunk * 64 - 6 + (lane >> 3);
-  const bool chroma = (pb - 6 * (pb / 6)) >= 4;
+  const bool chroma = desc_tab(desc[block_in_mcu(g, chunk * 64 - 8 + (lane >> 3))]) != 0;
   int sum = 0;
 #pragma unroll
   for (int x = 0; x < 8; x++) {
@@ -418,8 +448,8 @@ __device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, boo
   sum += __shfl_xor(sum, 1, 64);
   sum += __shfl_xor(sum, 2, 64);
   sum += __shfl_xor(sum, 4, 64);
-  const int d = __shfl((sum + 32) >> 6, max(lane - 58, 0) * 8, 64);
-  return lane >= 58 ? d : 128;
+  const int d = __shfl((sum + 32) >> 6, max(lane - 56, 0) * 8, 64);
+  return lane >= 56 ? d : 128;
 }
 
 // MODE: kEmitDefault (-huffman default, Annex K tables), kCount (-huffman optimal pass 1:
@@ -442,6 +472,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ __attribute__((aligned(16))) int s_m2[72];       // pass-2 dot rows + per-row constant
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
   __shared__ uint8_t s_rc[MJG_RC_LUT ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
+  __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   // per wave: the current frame's histogram (kCount) or code tables (kEmitFrame)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
@@ -456,7 +487,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_m2[tid] = kPass2Dot[tid];
     s_scat[tid] = kScreenScatter[tid];
   }
-  if (tid < 8) s_m2[64 + tid] = kPass2Add[tid];
+  if (tid < 8) {
+    s_m2[64 + tid] = kPass2Add[tid];
+    s_desc[tid] = tabs[672 + tid];
+  }
   if (MJG_RC_LUT && RC)
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
@@ -486,8 +520,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   } stamp_guard{stamp0, (uint64_t *)dbg_coefs + 2 * gw, lane};
 #endif
   if (gw >= nbatch) return;
-  const int nblk = g.nmcu * 6;
-  const int nck = (nblk + 63) >> 6;
+  const int nblk = g.seg_blocks;  // blocks of one entropy-coded segment
   constexpr bool rc = RC;
 
   // Batches of kBatch consecutive chunks: the first one static (batch gw), the rest
@@ -496,17 +529,19 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   int t = gw * kBatch, tend = min(t + kBatch, ntasks);
   uint32_t nb = 0;  // lane 0: the batch after this one
   if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
-  int frame = t / nck, chunk = t - frame * nck;
-  int b = chunk * 64 + lane;
+  int frame, chunk, bbase;
+  task_pos(g, t, frame, chunk, bbase);
+  int b = chunk * 64 + lane;  // block in the segment
   bool active = b < nblk;
   uint64_t raw[8];
-  bool fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
-  int carry = carry_finish(carry_row(frames, g, frame, chunk, lane), chunk, lane, rc);
+  bool fast = active && fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc));
+  int carry = carry_finish(carry_row(frames, g, frame, bbase, chunk, lane, s_desc), chunk, lane, rc, g,
+                           s_desc);
 
   while (true) {
-    const int blk = b - 6 * (b / 6);
-    const int tab = blk < 4 ? 0 : 1;
-    if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, b));
+    const uint32_t dsc = s_desc[block_in_mcu(g, b)];
+    const int tab = desc_tab(dsc);
+    if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, bbase + b, s_desc));
     // Row pass (jfdctint pass 1) in fp32, exactly: every value is an integer or a multiple
     // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
     // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
@@ -587,7 +622,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       __builtin_amdgcn_sched_barrier(0);
     }
     // prefetch the next chunk while this one is encoded
-    const int cur_frame = frame, cur_chunk = chunk;
+    const int cur_frame = frame, cur_chunk = chunk, cur_bbase = bbase;
     const bool cur_active = active;
     int tn = t + 1;
     const bool new_batch = tn >= tend;
@@ -596,14 +631,13 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       tn = nbu < nbatch ? nbu * kBatch : -1;
     }
     if (tn >= 0) {
-      frame = tn / nck;
-      chunk = tn - frame * nck;
+      task_pos(g, tn, frame, chunk, bbase);
       b = chunk * 64 + lane;
       active = b < nblk;
-      fast = active && fetch_rows(raw, block_src(frames, g, frame, b));
+      fast = active && fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc));
     }
     // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
-    const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, chunk, lane) : 0;
+    const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, bbase, chunk, lane, s_desc) : 0;
 
     // Column pass (jfdctint pass 2) as a float *screen*: the products of pass 2 need up to
     // 31 bits, so fp32 sums are only approximate (|error| < 2^9 before the 2^17 descale).
@@ -668,7 +702,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
         }
       }
       if (g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
-        uint32_t *dst = (uint32_t *)(dbg_coefs + ((size_t)cur_frame * nblk + cur_chunk * 64 + lane) * 64);
+        uint32_t *dst = (uint32_t *)(dbg_coefs +
+                                     ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
 #pragma unroll 1
         for (int n = 0; n < 64; n += 2) {
           const int a0 = n == 0 ? dc : exact_coef(s_pk + lane, n, s_m2, s_qc);
@@ -690,9 +725,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       mask |= 1ull << s_scat[32 + pos];
     }
 
-    // DC predictor (FFmpeg last_dc, 128 at every frame start): shuffle within the chunk,
+    // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.
-    const int delta = blk == 0 ? 3 : (blk < 4 ? 1 : 6);
+    const int delta = desc_delta(dsc);
     const int src_lane = (lane - delta) & 63;
     const int from_cur = __shfl(dc, src_lane, 64), from_prev = __shfl(carry, src_lane, 64);
     const int pred = lane >= delta ? from_cur : (cur_chunk == 0 ? 128 : from_prev);
@@ -722,7 +757,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       }
       if (tn < 0) break;
       if (new_batch) {
-        carry = carry_finish(crow, chunk, lane, rc);
+        carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
         tend = min(tn + kBatch, ntasks);
         if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
       }
@@ -806,7 +841,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     if (lane == 0) chunk_bits[t] = total;
     if (tn < 0) break;
     if (new_batch) {
-      carry = carry_finish(crow, chunk, lane, rc);
+      carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
       tend = min(tn + kBatch, ntasks);
       if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
     }
@@ -1225,8 +1260,28 @@ __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ g
   }
 }
 
+// RST mode (one entropy-coded segment per MCU row): per frame, the segments' offsets after
+// the header (exclusive scan of their stuffed sizes, each including its 2-byte trailer:
+// RSTn, or EOI for the last) and the frame size = header + all segments.
+__global__ __launch_bounds__(64) void k_seg_sizes(const uint64_t *__restrict__ seg_size, int nseg,
+                                                  int hdr_len, uint32_t *__restrict__ seg_off,
+                                                  uint64_t *__restrict__ frame_size) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  uint32_t carry = 0;
+  for (int s0 = 0; s0 < nseg; s0 += 64) {
+    const int s = s0 + lane;
+    const uint32_t v = s < nseg ? (uint32_t)seg_size[(size_t)f * nseg + s] : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (s < nseg) seg_off[(size_t)f * nseg + s] = carry + incl - v;
+    carry += __shfl(incl, 63, 64);
+  }
+  if (lane == 0) frame_size[f] = (uint64_t)hdr_len + carry;
+}
+
 // One wave per frame: packed output offset (sum of the preceding frame sizes), capacity
-// check, header (SOI .. SOS) and EOI of the frame.  -huffman optimal (hdr_lens != null):
+// check, header (SOI .. SOS) and EOI of the frame; in RST mode (seg_off != null) also the
+// RST0..7 marker closing every segment but the last (mjpegenc.c ff_mjpeg_encode_stuffing:
+// RST0 + (mb_y & 7) after MCU row mb_y).  -huffman optimal (hdr_lens != null):
 // the default header's bytes before and after its DHT around the frame's own DHT
 // (jpeg_table_header: one DHT, tables DC0, DC1, AC0, AC1).
 __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ frame_size,
@@ -1236,7 +1291,9 @@ __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ f
                                                   uint32_t *__restrict__ status,
                                                   const uint32_t *__restrict__ hdr_lens, int dht_pos,
                                                   int dht_end, const uint8_t *__restrict__ dht,
-                                                  const uint32_t *__restrict__ dht_nval) {
+                                                  const uint32_t *__restrict__ dht_nval,
+                                                  const uint32_t *__restrict__ seg_off,
+                                                  const uint64_t *__restrict__ seg_size, int nseg) {
   const int f = blockIdx.x, lane = threadIdx.x;
   uint64_t s = 0;
   for (int i = lane; i < f; i += 64) s += frame_size[i];
@@ -1280,6 +1337,13 @@ __global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ f
     fo[fsize - 2] = 0xff;
     fo[fsize - 1] = 0xd9;
   }
+  if (seg_off)
+    for (int sg = lane; sg < nseg - 1; sg += 64) {
+      const size_t i = (size_t)f * nseg + sg;
+      uint8_t *m = fo + hdr_len + seg_off[i] + seg_size[i] - 2;
+      m[0] = 0xff;
+      m[1] = (uint8_t)(0xd0 + (sg & 7));
+    }
 }
 
 // Wave per chunk group, lanes = words: the group's owned bytes with a 0x00 after every
@@ -1290,14 +1354,17 @@ __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
     const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
     const uint64_t *__restrict__ frame_offsets, int hdr_len, const uint32_t *__restrict__ hdr_lens,
-    int nchunks, int ngroups_per_frame, int ngroups, uint8_t *__restrict__ out, uint64_t out_cap) {
+    int nchunks, int ngroups_per_frame, int ngroups, uint8_t *__restrict__ out, uint64_t out_cap,
+    const uint32_t *__restrict__ seg_off, int nseg) {
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (gi >= ngroups) return;
+  // g.f is the entropy-coded segment (the frame itself unless RST mode)
   const GroupWords g = group_words(chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
-  const uint64_t foff = frame_offsets[g.f];
-  if (foff + frame_size[g.f] > out_cap) return;  // k_frame_hdr flagged the overflow
-  const uint32_t hl = hdr_lens ? hdr_lens[g.f] : (uint32_t)hdr_len;
-  uint8_t *base = out + foff + hl + 4 * (size_t)g.k0 + ff_off[gi];
+  const int fr = g.f / nseg;
+  const uint64_t foff = frame_offsets[fr];
+  if (foff + frame_size[fr] > out_cap) return;  // k_frame_hdr flagged the overflow
+  const uint32_t hl = hdr_lens ? hdr_lens[fr] : (uint32_t)hdr_len;
+  uint8_t *base = out + foff + hl + (seg_off ? seg_off[g.f] : 0u) + 4 * (size_t)g.k0 + ff_off[gi];
   uint32_t carry = 0;
   for (uint32_t kb = g.k0; kb < g.k1; kb += 64) {
     const uint32_t k = kb + lane;

@@ -1,10 +1,12 @@
 """GPU MJPEG encoder: the per-segment encode that the reference's worker runs
 (`ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:`,
 ffmpeg_distributed.py:131-141), restricted to the profile
-`[-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int [-huffman default|optimal] -bitexact`.
+`[-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int [-huffman default|optimal] -bitexact`
+(+ `-slices N` / `-thread_type slice` for the RST layout).
 
-Host-side wrapper over libmjgpu.so; frames are packed I420 (yuv420p / yuvj420p), i.e.
-what `ffmpeg -f rawvideo -pix_fmt yuv420p` writes.  No CPU fallback.
+Host-side wrapper over libmjgpu.so; frames are packed planar YUV (yuv420p / yuvj420p by
+default, 4:2:2 and 4:4:4 with `chroma=`), i.e. what `ffmpeg -f rawvideo -pix_fmt yuv4xxp`
+writes.  No CPU fallback.
 """
 from __future__ import annotations
 
@@ -17,13 +19,23 @@ from . import _lib
 from ._lib import MjgConfig, MjgError, check
 
 
-def i420_frame_bytes(w: int, h: int) -> int:
-    return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
+CHROMA_SHIFTS = {"420": (1, 1), "422": (1, 0), "444": (0, 0)}
 
 
-def split_i420(frame: np.ndarray, w: int, h: int):
-    """Views (Y, U, V) of one packed I420 frame."""
-    cw, ch = (w + 1) // 2, (h + 1) // 2
+def chroma_size(w: int, h: int, chroma: str = "420"):
+    """(width, height) of a chroma plane: ((w + hs) >> hs, (h + vs) >> vs)."""
+    hs, vs = CHROMA_SHIFTS[str(chroma)]
+    return (w + hs) >> hs, (h + vs) >> vs
+
+
+def i420_frame_bytes(w: int, h: int, chroma: str = "420") -> int:
+    cw, ch = chroma_size(w, h, chroma)
+    return w * h + 2 * cw * ch
+
+
+def split_i420(frame: np.ndarray, w: int, h: int, chroma: str = "420"):
+    """Views (Y, U, V) of one packed planar frame (I420 unless `chroma` says otherwise)."""
+    cw, ch = chroma_size(w, h, chroma)
     f = np.asarray(frame, dtype=np.uint8).reshape(-1)
     y = f[: w * h].reshape(h, w)
     u = f[w * h: w * h + cw * ch].reshape(ch, cw)
@@ -42,7 +54,7 @@ class MjpegEncoder:
                  dst_h: Optional[int] = None, full_range: bool = False, qscale: int = 5,
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
                  debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
-                 huffman: str = "default"):
+                 huffman: str = "default", chroma: str = "420", rst: bool = False):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -62,10 +74,17 @@ class MjpegEncoder:
             flags |= _lib.MJG_F_HUFFMAN_OPTIMAL
         elif huffman != "default":
             raise ValueError(f"huffman {huffman!r}")
+        if rst:
+            flags |= _lib.MJG_F_RST
         self.huffman = huffman
+        self.chroma = str(chroma)
+        if self.chroma not in _lib.CHROMA_FORMATS:
+            raise ValueError(f"chroma {chroma!r}")
+        self.rst = bool(rst)
         sar = sar or (0, 0)
         cfg = MjgConfig(self.src_w, self.src_h, self.dst_w, self.dst_h, int(bool(full_range)),
-                        int(qscale), int(sar[0]), int(sar[1]), self.max_batch, flags)
+                        int(qscale), int(sar[0]), int(sar[1]), self.max_batch, flags,
+                        _lib.CHROMA_FORMATS[self.chroma])
         h = C.c_void_p()
         check(self._L.mjg_open(self.device, C.byref(cfg), C.byref(h)))
         self._h = h
@@ -117,7 +136,7 @@ class MjpegEncoder:
                                    else np.asarray(frames, dtype=np.uint8))
         if arr.size % self.frame_bytes:
             raise ValueError(f"buffer of {arr.size} bytes is not a whole number of "
-                             f"{self.frame_bytes}-byte I420 frames")
+                             f"{self.frame_bytes}-byte frames")
         n = arr.size // self.frame_bytes if nframes is None else int(nframes)
         self._keep = arr  # the async H2D copy reads it until sync()
         check(self._L.mjg_submit(self._h, C.c_void_p(arr.ctypes.data), n, 0))
@@ -165,14 +184,15 @@ class MjpegEncoder:
         return {k: ms[i] for i, k in enumerate(_lib.KERNEL_NAMES)}, n.value
 
     def debug_coefs(self, frame: int = 0) -> np.ndarray:
-        nmcu = ((self.dst_w + 15) // 16) * ((self.dst_h + 15) // 16)
-        out = np.zeros((nmcu * 6, 64), np.int16)
+        mcu_w = 8 if self.chroma == "444" else 16
+        nmcu = ((self.dst_w + mcu_w - 1) // mcu_w) * ((self.dst_h + 15) // 16)
+        out = np.zeros((nmcu * (8 if self.chroma == "422" else 6), 64), np.int16)
         check(self._L.mjg_debug_coefs(self._h, int(frame), out.ctypes.data_as(C.POINTER(C.c_int16)),
                                       out.shape[0]))
         return out
 
     def debug_planes(self, frame: int = 0) -> np.ndarray:
-        n = i420_frame_bytes(self.dst_w, self.dst_h)
+        n = i420_frame_bytes(self.dst_w, self.dst_h, self.chroma)
         out = np.zeros(n, np.uint8)
         check(self._L.mjg_debug_planes(self._h, int(frame), out.ctypes.data_as(C.POINTER(C.c_uint8)), n))
         return out

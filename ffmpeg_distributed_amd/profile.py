@@ -4,8 +4,14 @@ arguments fall outside it (the worker then runs the real ffmpeg unchanged).
 
 Supported profile (BASELINE north star, plus FFmpeg's default -huffman optimal):
     [-vf scale=W:H[:flags=bicubic...]] -c:v mjpeg -q:v N -dct int [-huffman default|optimal] -bitexact
-plus options that do not change the video bitstream: -an -sn -dn -y -threads N
--pix_fmt yuvj420p -f matroska -map 0:v[:0].
+plus
+  - the slice-threaded (RST) layout: -slices N (N > 1), or -thread_type slice with -threads
+    other than 1 (mpegvideo's slice_context_count > 1: DRI + one restart interval per MCU
+    row; mjpegenc.c then forces -huffman default);
+  - -pix_fmt yuvj420p / yuvj422p / yuvj444p (the output sampling; the worker checks it
+    against the input's, since a chroma resample is not on the GPU path);
+  - options that do not change the video bitstream: -an -sn -dn -y -threads N
+    -thread_type frame -f matroska -map 0:v[:0].
 """
 from __future__ import annotations
 
@@ -22,6 +28,8 @@ class Profile:
     scale: Optional[Tuple[int, int]] = None   # -vf scale=W:H
     sws_flags: Tuple[str, ...] = ("bicubic",)
     huffman: str = "optimal"         # mjpegenc.c "huffman" option, default optimal
+    rst: bool = False                # slice threading: DRI + RST per MCU row
+    chroma: Optional[str] = None     # "420"/"422"/"444" from -pix_fmt (None: the input's)
 
 
 class Unsupported(ValueError):
@@ -70,6 +78,10 @@ def parse(args: Union[str, Sequence[str]]) -> Profile:
     a: List[str] = shlex.split(args) if isinstance(args, str) else list(args)
     codec = q = dct = huff = None
     bitexact = False
+    slices = 0
+    threads: Optional[int] = None     # None: auto (0)
+    thread_type = "slice+frame"       # AVCodecContext default: FF_THREAD_FRAME | FF_THREAD_SLICE
+    chroma = None
     scale = None
     flags: Tuple[str, ...] = ("bicubic",)
     i = 0
@@ -106,11 +118,28 @@ def parse(args: Union[str, Sequence[str]]) -> Profile:
             scale, flags = _parse_scale(val())
         elif o in ("-an", "-sn", "-dn", "-y"):
             pass
-        elif o == "-threads":
-            val()
-        elif o == "-pix_fmt":
-            if val() not in ("yuvj420p",):
-                raise Unsupported(f"-pix_fmt {a[i]} (GPU path writes 4:2:0 full range)")
+        elif o in ("-threads", "-threads:v"):
+            v = val()
+            try:
+                threads = None if v == "auto" else int(v)
+            except ValueError:
+                raise Unsupported(f"{o} {v}")
+            if threads == 0:
+                threads = None
+        elif o in ("-thread_type", "-thread_type:v"):
+            thread_type = val()
+            if any(t not in ("slice", "frame") for t in thread_type.split("+")):
+                raise Unsupported(f"-thread_type {thread_type}")
+        elif o in ("-slices", "-slices:v"):
+            try:
+                slices = int(val())
+            except ValueError:
+                raise Unsupported(f"-slices {a[i]}")
+        elif o in ("-pix_fmt", "-pix_fmt:v"):
+            pf = val()
+            if pf not in PIX_FMT_CHROMA:
+                raise Unsupported(f"-pix_fmt {pf} (GPU path writes yuvj420p/422p/444p)")
+            chroma = PIX_FMT_CHROMA[pf]
         elif o == "-f":
             if val() != "matroska":
                 raise Unsupported(f"-f {a[i]}")
@@ -132,7 +161,29 @@ def parse(args: Union[str, Sequence[str]]) -> Profile:
         raise Unsupported(f"-huffman {huff!r}")
     if not bitexact:
         raise Unsupported("no -bitexact (the Lavc COM segment is build-specific)")
-    return Profile(qscale=effective_qscale(q), q_arg=q, scale=scale, sws_flags=flags, huffman=huff)
+    rst = uses_slices(slices, threads, thread_type)
+    if rst:
+        huff = "default"  # mjpegenc.c: slice_context_count > 1 forces HUFFMAN_TABLE_DEFAULT
+    return Profile(qscale=effective_qscale(q), q_arg=q, scale=scale, sws_flags=flags, huffman=huff,
+                   rst=rst, chroma=chroma)
+
+
+PIX_FMT_CHROMA = {"yuvj420p": "420", "yuvj422p": "422", "yuvj444p": "444"}
+
+
+def uses_slices(slices: int, threads: Optional[int], thread_type: str) -> bool:
+    """Whether the mjpeg encoder runs with slice_context_count > 1 (mpegvideo.c
+    ff_mpv_init_context: nb_slices = -slices if set, else the thread count when slice
+    threading is active; the frame-threading encoder, preferred whenever "frame" is in
+    -thread_type, gives each frame a single-threaded context).  The layout then does not
+    depend on the slice count (a restart interval per MCU row either way); -threads auto
+    counts as more than one thread.  A one-MCU-row picture still gets no RST (the slice
+    count is clipped to mb_height), which the encoder handles."""
+    if slices:
+        return slices > 1
+    if threads == 1:
+        return False
+    return "frame" not in thread_type.split("+")
 
 
 def av_reduce(num: int, den: int, max_v: int) -> Tuple[int, int]:

@@ -9,9 +9,11 @@ lines on stderr (parsed at ffmpeg_distributed.py:39-40,62-73), exit code 0 on su
 remote_args inside the GPU profile (profile.parse) are encoded on GPU N; anything else
 runs the reference command line with the real ffmpeg as a child (same output, CPU).
 
-Input: Matroska with V_UNCOMPRESSED I420 video and YUV4MPEG2 are read natively; any
-other codec (the splitter's lossless x264 segments, fd.py:198-202) is decoded by an
+Input: Matroska with V_UNCOMPRESSED I420/Y42B/444P video and YUV4MPEG2 are read natively;
+any other codec (the splitter's lossless x264 segments, fd.py:198-202) is decoded by an
 `ffmpeg ... -f yuv4mpegpipe` child feeding this process (SURVEY §8f "splitter decode").
+A -pix_fmt whose sampling differs from the input's needs a chroma resample, which is not on
+the GPU path: the decoded frames then go to the real ffmpeg as y4m (`ffmpeg_fallthrough`).
 """
 from __future__ import annotations
 
@@ -77,7 +79,7 @@ class Progress:
 
 
 class Source:
-    """Packed I420 frames from stdin: .info (StreamInfo), .read_into(buf, n) -> count."""
+    """Packed planar frames from stdin: .info (StreamInfo), .read_into(buf, n) -> count."""
 
     def __init__(self, raw):
         self.child = None
@@ -95,7 +97,7 @@ class Source:
             raise ValueError("no video track in the segment")
         self.duration = mkv.duration_seconds()
         info = mkv.info(tr.number)
-        if tr.codec == "V_UNCOMPRESSED" and tr.colour_space in (b"I420", b""):
+        if tr.codec == "V_UNCOMPRESSED" and tr.colour_space in container.MKV_FOURCC_CHROMA:
             self.info = info
             self._frames = mkv.frames(tr.number)
             self.read_into = self._read_mkv
@@ -136,7 +138,7 @@ class Source:
             except StopIteration:
                 return i
             if len(data) != fb:
-                raise ValueError(f"V_UNCOMPRESSED frame of {len(data)} bytes, expected I420 {fb}")
+                raise ValueError(f"V_UNCOMPRESSED frame of {len(data)} bytes, expected {fb}")
             mv[i * fb:(i + 1) * fb] = data
         return n
 
@@ -156,6 +158,34 @@ def passthrough(args: List[str]) -> int:
         return 127
 
 
+def ffmpeg_fallthrough(src: Source, args: List[str], stdout) -> int:
+    """The reference command on the CPU for frames already being read: the decoded frames
+    go to `ffmpeg -f yuv4mpegpipe -i pipe: <remote_args> -f matroska pipe:` as y4m."""
+    argv = ["ffmpeg", "-f", "yuv4mpegpipe", "-i", "pipe:", *args, "-f", "matroska", "pipe:"]
+    try:
+        child = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=stdout)
+    except FileNotFoundError:
+        sys.stderr.write("ffmpeg not found for a non-GPU profile\n")
+        src.close()
+        return 127
+    fb = src.info.frame_bytes
+    buf = bytearray(fb * 8)
+    try:
+        child.stdin.write(container.y4m_header(src.info))
+        while True:
+            n = src.read_into(buf, 8)
+            for i in range(n):
+                child.stdin.write(b"FRAME\n")
+                child.stdin.write(memoryview(buf)[i * fb:(i + 1) * fb])
+            if n < 8:
+                break
+        child.stdin.close()
+    except BrokenPipeError:
+        pass
+    rc = child.wait()
+    return rc or src.close()
+
+
 def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> int:
     stdin = stdin or sys.stdin.buffer
     stdout = stdout or sys.stdout.buffer
@@ -168,13 +198,19 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
 
     src = Source(stdin)
     info = src.info
+    if prof.chroma is not None and prof.chroma != info.chroma:
+        stderr.write(f"gpu:{device}: -pix_fmt needs {info.chroma} -> {prof.chroma} chroma resampling; "
+                     f"running ffmpeg on the CPU\n")
+        stderr.flush()
+        return ffmpeg_fallthrough(src, args, stdout)
     dst_w, dst_h = prof.scale or (info.width, info.height)
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
                        qscale=prof.qscale, sar=sar, max_batch=BATCH,
-                       com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman)
+                       com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman,
+                       chroma=info.chroma, rst=prof.rst)
     prog = Progress(stderr, info.fps, prof.qscale)
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)

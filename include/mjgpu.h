@@ -46,6 +46,17 @@ extern "C" {
 #define MJG_F_HUFFMAN_OPTIMAL 16u /* -huffman optimal (FFmpeg's default): per-frame Huffman tables
                                   from the frame's symbol counts (mjpegenc_huffman.c); the
                                   header's DHT then differs per frame */
+#define MJG_F_RST 32u          /* slice-threaded bitstream (-slices N / -thread_type slice): DRI =
+                                  MCUs per row, every MCU row its own entropy-coded segment
+                                  (DC predictors reset, 1-bit padded, RST0..7 between rows;
+                                  mpegvideo_enc.c encode_thread rtp_mode + mjpegenc.c
+                                  ff_mjpeg_encode_stuffing).  Implies -huffman default, as
+                                  FFmpeg forces; MJG_F_RST | MJG_F_HUFFMAN_OPTIMAL is invalid */
+
+/* mjg_config.chroma_format */
+#define MJG_CHROMA_420 0       /* yuv(j)420p: MCU 16x16, Y 2x2 Cb 1x1 Cr 1x1 */
+#define MJG_CHROMA_422 1       /* yuv(j)422p: MCU 16x16, Y 2x2 Cb 1x2 Cr 1x2 */
+#define MJG_CHROMA_444 2       /* yuv(j)444p: MCU 8x16, every component 1x2 (ff_mjpeg_init_hvsample) */
 
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane)        */
@@ -65,6 +76,7 @@ typedef struct mjg_config {
   int32_t sar_num, sar_den;  /* JFIF APP0 density; 0/0 omits APP0 (unknown SAR)        */
   int32_t max_batch;         /* most frames one mjg_submit() may carry                 */
   uint32_t flags;            /* MJG_F_*                                                */
+  int32_t chroma_format;     /* MJG_CHROMA_*; frames are packed planar Y, Cb, Cr       */
 } mjg_config;
 
 typedef struct mjg_ctx mjg_ctx;
@@ -83,7 +95,7 @@ int mjg_device_count(void);
 int mjg_open(int device, const mjg_config *cfg, mjg_ctx **out);
 void mjg_close(mjg_ctx *ctx);
 
-/* Bytes of one packed I420 input frame (src_w x src_h). */
+/* Bytes of one packed planar input frame (src_w x src_h in cfg->chroma_format). */
 size_t mjg_frame_bytes(const mjg_ctx *ctx);
 /* The per-config JPEG header (SOI .. SOS) every frame starts with.  With
  * MJG_F_HUFFMAN_OPTIMAL each frame carries its own DHT; this returns the header with the
@@ -117,7 +129,8 @@ int mjg_host_free(void *ptr);
 int mjg_kernel_times(mjg_ctx *ctx, double *ms /* [MJG_NUM_KERNELS] */, int *launches, int reset);
 
 /* Device-free helpers (no HIP call; usable on a host without a GPU). */
-/* The per-config JPEG header (SOI .. SOS) for cfg (only dst_w/dst_h/qscale/sar are read). */
+/* The per-config JPEG header (SOI .. SOS) for cfg (dst_w/dst_h/qscale/sar/chroma_format and the
+ * MJG_F_COM_ITU601 / MJG_F_RST flags are read). */
 int mjg_build_header(const mjg_config *cfg, uint8_t *out, size_t cap, size_t *len);
 /* swscale bicubic filter table the scale stage applies: one = 1<<14 (horizontal) or 1<<12
  * (vertical); align = 4 / 2 (x86 swscale); pos = swscale local position (128 = centred).
@@ -127,10 +140,10 @@ int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, i
 
 /* Test hooks (tests/ only). */
 /* Quantized coefficients (natural order) of frame `frame` of the last submit, blocks
- * in MCU order (Y0 Y1 Y2 Y3 Cb Cr per MCU).  Needs MJG_F_DEBUG_COEFS. */
+ * in coding order (4:2:0: Y0 Y1 Y2 Y3 Cb Cr per MCU).  Needs MJG_F_DEBUG_COEFS. */
 int mjg_debug_coefs(mjg_ctx *ctx, int frame, int16_t *out, size_t nblocks);
 /* The full-range encoder-input planes (after scale/range stage) of frame `frame`,
- * packed I420 at dst size.  Only meaningful when the config scales. */
+ * packed planar at dst size.  Only meaningful when the config scales. */
 int mjg_debug_planes(mjg_ctx *ctx, int frame, uint8_t *out, size_t cap);
 /* Filter tables the context generated: plane 0 = luma, 1 = chroma; dir 0 = horizontal,
  * 1 = vertical.  taps/len may be queried with coeff == NULL. */

@@ -5,7 +5,8 @@
  * external `ffmpeg` worker (ffmpeg_distributed.py:131-141 spawns
  * `ffmpeg -f matroska -i pipe: <remote_args> -f matroska pipe:`), restricted to the
  * north-star profile  [-vf scale=W:H:flags=bicubic] -c:v mjpeg -q:v N -dct int
- * -huffman default|optimal -bitexact  on yuv420p / yuvj420p frames.
+ * -huffman default|optimal -bitexact  on yuv420p / yuvj420p frames, plus the 4:2:2 / 4:4:4
+ * variants and the RST (slice-threaded) bitstream layout.
  *
  * The arithmetic lives in third-party FFmpeg (libavcodec mjpeg encoder, libswscale),
  * which is NOT vendored under /root/reference, not pinned by it (no requirements
@@ -374,9 +375,10 @@ static void or_count_block(uint32_t counts[4][256], const int16_t *block, int n,
 
 /* ---------------------------------------------------------------- header */
 /* mjpegenc_common.c ff_mjpeg_encode_picture_header + jpeg_put_comments +
- * jpeg_table_header, for AV_CODEC_ID_MJPEG, 4:2:0, -bitexact (no COM Lavc),
- * -huffman default, equal luma/chroma matrices (one DQT table), frame threads
- * (no DRI).  com_itu601: the COM "CS=ITU601" segment for limited-range input. */
+ * jpeg_table_header, for AV_CODEC_ID_MJPEG, -bitexact (no COM Lavc), equal luma/chroma
+ * matrices (one DQT table); SOF0 sampling factors from ff_mjpeg_init_hvsample; DRI only
+ * with slice threading (dri_interval > 0, written after DQT and before DHT).
+ * com_itu601: the COM "CS=ITU601" segment for limited-range input. */
 static void put16(or_pb *pb, int v) { pb_put(pb, 16, (uint32_t)v & 0xffff); }
 static void put8(or_pb *pb, int v) { pb_put(pb, 8, (uint32_t)v & 0xff); }
 
@@ -389,10 +391,13 @@ static int put_huffman_table(or_pb *pb, int cls, int id, const uint8_t *bits, co
     return n + 17;
 }
 
-static size_t or_header_tables(int width, int height, int qscale, int sar_num, int sar_den,
-                               int com_itu601, int dri_interval, const uint8_t *const bits[4],
-                               const uint8_t *const vals[4], uint8_t *out, size_t cap)
+static void or_hvsample(int cfmt, int hs[3], int vs[3]);
+static size_t or_header_fmt(int width, int height, int cfmt, int qscale, int sar_num, int sar_den,
+                            int com_itu601, int dri_interval, const uint8_t *const bits[4],
+                            const uint8_t *const vals[4], uint8_t *out, size_t cap)
 {
+    int hs[3], vs[3];
+    or_hvsample(cfmt, hs, vs);
     or_pb pb = { out, cap, 0, 0 };
     uint8_t mprime[64]; int32_t qmat[64];
     or_build_matrix(qscale, mprime, qmat);
@@ -427,9 +432,9 @@ static size_t or_header_tables(int width, int height, int qscale, int sar_num, i
     if (len_pos + 1 < cap) { out[len_pos] = (uint8_t)(size >> 8); out[len_pos + 1] = (uint8_t)size; }
     put16(&pb, 0xFFC0); put16(&pb, 17); put8(&pb, 8);   /* SOF0 */
     put16(&pb, height); put16(&pb, width); put8(&pb, 3);
-    put8(&pb, 1); pb_put(&pb, 4, 2); pb_put(&pb, 4, 2); put8(&pb, 0);
-    put8(&pb, 2); pb_put(&pb, 4, 1); pb_put(&pb, 4, 1); put8(&pb, 0);
-    put8(&pb, 3); pb_put(&pb, 4, 1); pb_put(&pb, 4, 1); put8(&pb, 0);
+    for (int c = 0; c < 3; c++) {                        /* id, HxV, Tq 0 (one matrix) */
+        put8(&pb, c + 1); pb_put(&pb, 4, hs[c]); pb_put(&pb, 4, vs[c]); put8(&pb, 0);
+    }
     put16(&pb, 0xFFDA); put16(&pb, 6 + 2 * 3); put8(&pb, 3);  /* SOS */
     put8(&pb, 1); pb_put(&pb, 4, 0); pb_put(&pb, 4, 0);
     put8(&pb, 2); pb_put(&pb, 4, 1); pb_put(&pb, 4, 1);
@@ -437,6 +442,25 @@ static size_t or_header_tables(int width, int height, int qscale, int sar_num, i
     put8(&pb, 0); put8(&pb, 63); put8(&pb, 0);
     if (pb.overflow) return 0;
     return pb.nbits >> 3;
+}
+
+/* mjpegenc_common.c ff_mjpeg_init_hvsample: (h, v) sampling factors of Y, Cb, Cr.
+ * cfmt 0 = 4:2:0, 1 = 4:2:2, 2 = 4:4:4 (the 4:4:4 special case: every component 1x2, so an
+ * MCU is 8x16 pixels). */
+static void or_hvsample(int cfmt, int hs[3], int vs[3])
+{
+    if (cfmt == 2) { hs[0] = hs[1] = hs[2] = 1; vs[0] = vs[1] = vs[2] = 2; return; }
+    hs[0] = 2; vs[0] = 2;
+    hs[1] = hs[2] = 1;
+    vs[1] = vs[2] = cfmt == 1 ? 2 : 1;
+}
+
+static size_t or_header_tables(int width, int height, int qscale, int sar_num, int sar_den,
+                               int com_itu601, int dri_interval, const uint8_t *const bits[4],
+                               const uint8_t *const vals[4], uint8_t *out, size_t cap)
+{
+    return or_header_fmt(width, height, 0, qscale, sar_num, sar_den, com_itu601, dri_interval,
+                         bits, vals, out, cap);
 }
 
 static const uint8_t *const or_default_bits[4] = { or_bits_dc_lum, or_bits_dc_chr, or_bits_ac_lum, or_bits_ac_chr };
@@ -447,6 +471,19 @@ size_t or_header(int width, int height, int qscale, int sar_num, int sar_den, in
 {
     return or_header_tables(width, height, qscale, sar_num, sar_den, com_itu601, dri_interval,
                             or_default_bits, or_default_vals, out, cap);
+}
+
+/* The header for chroma format cfmt; rst != 0 adds the DRI segment slice threading writes
+ * (jpeg_table_header: interval (width - 1) / (8 * hsample[0]) + 1 = MCUs per MCU row). */
+size_t or_header_cfmt(int width, int height, int cfmt, int qscale, int sar_num, int sar_den,
+                      int com_itu601, int rst, uint8_t *out, size_t cap)
+{
+    int hs[3], vs[3];
+    if (cfmt < 0 || cfmt > 2) return 0;
+    or_hvsample(cfmt, hs, vs);
+    return or_header_fmt(width, height, cfmt, qscale, sar_num, sar_den, com_itu601,
+                         rst ? (width - 1) / (8 * hs[0]) + 1 : 0, or_default_bits, or_default_vals,
+                         out, cap);
 }
 
 /* ------------------------------------------------- -huffman optimal tables */
@@ -645,90 +682,172 @@ static void or_get_block(int16_t *blk, const uint8_t *plane, int stride, int pw,
     }
 }
 
-/* Quantized coefficients of every block of one 4:2:0 frame, natural order, in
- * MCU order (Y0 Y1 Y2 Y3 Cb Cr per MCU), plus last_index per block.  Exposed so
- * the GPU's intermediate products can be compared block by block. */
-int or_frame_coeffs(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
-                    int w, int h, int qscale, int16_t *coef_out, int8_t *last_out)
+/* MCU layouts per chroma format (cfmt 0 = 4:2:0, 1 = 4:2:2, 2 = 4:4:4).
+ * mpegvideo_enc.c encode_mb_internal numbers a 16x16 macroblock's blocks 0-3 = Y TL TR BL
+ * BR, 4/5 = Cb/Cr top (left), 6/7 = Cb/Cr bottom (4:2:2) or right (4:4:4), 8-11 = Cb/Cr
+ * bottom-left, Cb/Cr bottom-right (4:4:4); mjpegenc.c ff_mjpeg_encode_mb codes them as
+ *   4:2:0  0 1 2 3 4 5             (MCU 16x16: Y 2x2, Cb 1x1, Cr 1x1)
+ *   4:2:2  0 1 2 3 4 6 5 7         (MCU 16x16: Y 2x2, Cb 1x2, Cr 1x2)
+ *   4:4:4  0 2 4 8 5 9 | 1 3 6 10 7 11   (two 8x16 MCUs per macroblock, every component 1x2;
+ *          the right one only when 16*mb_x + 8 < width)
+ * so in MCU units every format is a raster of MCUs of `bpm` blocks whose (plane, dx, dy)
+ * is fixed; `n` is FFmpeg's block number, which selects the component (n < 4: Y, else
+ * (n & 1) + 1) and the Huffman table in encode_block. */
+typedef struct { int n, plane, dx, dy; } or_blk;
+typedef struct { int bpm, mcu_w[3], mcu_h[3], hshift, vshift; or_blk b[8]; } or_layout;
+static const or_layout or_layouts[3] = {
+    { 6, { 16, 8, 8 }, { 16, 8, 8 }, 1, 1,
+      { { 0, 0, 0, 0 }, { 1, 0, 8, 0 }, { 2, 0, 0, 8 }, { 3, 0, 8, 8 }, { 4, 1, 0, 0 }, { 5, 2, 0, 0 } } },
+    { 8, { 16, 8, 8 }, { 16, 16, 16 }, 1, 0,
+      { { 0, 0, 0, 0 }, { 1, 0, 8, 0 }, { 2, 0, 0, 8 }, { 3, 0, 8, 8 }, { 4, 1, 0, 0 }, { 6, 1, 0, 8 },
+        { 5, 2, 0, 0 }, { 7, 2, 0, 8 } } },
+    { 6, { 8, 8, 8 }, { 16, 16, 16 }, 0, 0,
+      { { 0, 0, 0, 0 }, { 2, 0, 0, 8 }, { 4, 1, 0, 0 }, { 8, 1, 0, 8 }, { 5, 2, 0, 0 }, { 9, 2, 0, 8 } } },
+};
+
+/* MCUs per row / per column of a w x h frame in chroma format cfmt. */
+void or_mcu_grid(int cfmt, int w, int h, int *mcw, int *mch)
 {
+    const or_layout *L = &or_layouts[cfmt];
+    *mcw = (w + L->mcu_w[0] - 1) / L->mcu_w[0];
+    *mch = (h + 15) / 16;
+}
+
+/* Quantized coefficients of every block of one frame in chroma format cfmt, natural
+ * order, in coding order (MCU raster, the layout's blocks per MCU), plus last_index per
+ * block.  Chroma planes are ((w + hshift) >> hshift) x ((h + vshift) >> vshift); partial
+ * MCUs replicate the plane's last row/column (emulated_edge_mc).  Exposed so the GPU's
+ * intermediate products can be compared block by block. */
+int or_frame_coeffs_cfmt(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                         int w, int h, int cfmt, int qscale, int16_t *coef_out, int8_t *last_out)
+{
+    if (cfmt < 0 || cfmt > 2) return -1;
+    const or_layout *L = &or_layouts[cfmt];
     uint8_t mprime[64]; int32_t qmat[64];
     or_build_matrix(qscale, mprime, qmat);
-    int mbw = (w + 15) / 16, mbh = (h + 15) / 16;
-    int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+    int mcw, mch;
+    or_mcu_grid(cfmt, w, h, &mcw, &mch);
+    const uint8_t *pl[3] = { y, u, v };
+    const int st[3] = { ys, us, vs };
+    const int pw[3] = { w, (w + L->hshift) >> L->hshift, (w + L->hshift) >> L->hshift };
+    const int ph[3] = { h, (h + L->vshift) >> L->vshift, (h + L->vshift) >> L->vshift };
     size_t b = 0;
-    for (int my = 0; my < mbh; my++)
-        for (int mx = 0; mx < mbw; mx++)
-            for (int n = 0; n < 6; n++, b++) {
+    for (int my = 0; my < mch; my++)
+        for (int mx = 0; mx < mcw; mx++)
+            for (int j = 0; j < L->bpm; j++, b++) {
+                const or_blk *d = &L->b[j];
                 int16_t *blk = coef_out + b * 64;
-                if (n < 4) or_get_block(blk, y, ys, w, h, mx * 16 + (n & 1) * 8, my * 16 + (n >> 1) * 8);
-                else if (n == 4) or_get_block(blk, u, us, cw, ch, mx * 8, my * 8);
-                else or_get_block(blk, v, vs, cw, ch, mx * 8, my * 8);
+                or_get_block(blk, pl[d->plane], st[d->plane], pw[d->plane], ph[d->plane],
+                             mx * L->mcu_w[d->plane] + d->dx, my * L->mcu_h[d->plane] + d->dy);
                 or_fdct_islow(blk);
                 last_out[b] = (int8_t)or_quantize(blk, qmat);
             }
     return 0;
 }
 
-/* ----------------------------------------------------------- full frame */
-/* mjpegenc_common.c ff_mjpeg_escape_FF + ff_mjpeg_encode_stuffing: pad the scan
- * with 1-bits to a byte boundary, insert 0x00 after every 0xFF of the scan data;
- * then EOI (ff_mjpeg_encode_picture_trailer). */
-size_t or_encode_planes_ex(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
-                           int w, int h, int qscale, int sar_num, int sar_den, int com_itu601,
-                           int huff_optimal, uint8_t *out, size_t cap)
+int or_frame_coeffs(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                    int w, int h, int qscale, int16_t *coef_out, int8_t *last_out)
 {
-    int mbw = (w + 15) / 16, mbh = (h + 15) / 16;
-    size_t nblocks = (size_t)mbw * mbh * 6;
+    return or_frame_coeffs_cfmt(y, ys, u, us, v, vs, w, h, 0, qscale, coef_out, last_out);
+}
+
+/* ----------------------------------------------------------- full frame */
+/* mjpegenc_common.c ff_mjpeg_escape_FF (+ the 1-bit padding of ff_mjpeg_encode_stuffing):
+ * pad the entropy-coded segment in seg to a byte boundary with 1-bits and append its bytes
+ * to out[*pos] with a 0x00 after every 0xFF.  Returns 0, or -1 on overflow. */
+static int or_flush_segment(or_pb *seg, uint8_t *out, size_t cap, size_t *pos)
+{
+    int pad = (int)((8 - (seg->nbits & 7)) & 7);
+    if (pad) pb_put(seg, pad, (1u << pad) - 1);
+    if (seg->overflow) return -1;
+    size_t size = seg->nbits >> 3;
+    for (size_t i = 0; i < size; i++) {
+        if (*pos + 2 > cap) return -1;
+        out[(*pos)++] = seg->buf[i];
+        if (seg->buf[i] == 0xFF) out[(*pos)++] = 0x00;
+    }
+    seg->nbits = 0;
+    return 0;
+}
+
+/* One frame in chroma format cfmt:
+ *   header (ff_mjpeg_encode_picture_header), scan, EOI (ff_mjpeg_encode_picture_trailer).
+ * rst = 0 (frame threading, the default): one entropy-coded segment, padded and escaped.
+ * rst = 1 (slice threading: -slices N or -thread_type slice; mpegvideo_enc.c sets rtp_mode
+ *   and encode_thread's MJPEG case starts a "GOB" at every mb_x == 0, mb_y != 0, i.e.
+ *   write_slice_end -> ff_mjpeg_encode_stuffing at the end of every MCU row): each MCU row
+ *   is its own segment -- padded with 1-bits, escaped, followed by RST0 + (row & 7) unless
+ *   it is the last row -- and the DC predictors restart at 128 in every row.  Slice
+ *   threading forces -huffman default (mjpegenc.c: slice_context_count > 1), so
+ *   huff_optimal with rst is rejected here.
+ * huff_optimal: mjpegenc.c ff_mjpeg_encode_stuffing -> mjpeg_build_optimal_huffman: the
+ *   picture's symbols are buffered, counted, and the tables built before the header and
+ *   the scan are written. */
+size_t or_encode_planes_cfmt(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                             int w, int h, int cfmt, int qscale, int sar_num, int sar_den, int com_itu601,
+                             int huff_optimal, int rst, uint8_t *out, size_t cap)
+{
+    if (cfmt < 0 || cfmt > 2 || (rst && huff_optimal)) return 0;
+    const or_layout *L = &or_layouts[cfmt];
+    int mcw, mch;
+    or_mcu_grid(cfmt, w, h, &mcw, &mch);
+    if (mch < 2) rst = 0;   /* mpegvideo: nb_slices is clipped to mb_height */
+    const int bpm = L->bpm;
+    size_t nblocks = (size_t)mcw * mch * bpm;
     int16_t *coef = (int16_t *)malloc(nblocks * 64 * sizeof(int16_t));
     int8_t *last = (int8_t *)malloc(nblocks);
-    if (!coef || !last) { free(coef); free(last); return 0; }
-    or_frame_coeffs(y, ys, u, us, v, vs, w, h, qscale, coef, last);
+    size_t seg_cap = nblocks * 210 + 64;     /* worst case ~1664 bits per block */
+    uint8_t *segbuf = (uint8_t *)malloc(seg_cap);
+    if (!coef || !last || !segbuf) { free(coef); free(last); free(segbuf); return 0; }
+    or_frame_coeffs_cfmt(y, ys, u, us, v, vs, w, h, cfmt, qscale, coef, last);
 
     const uint8_t *bits[4], *vals[4];
     uint8_t obits[4][17], ovals[4][256];
     for (int t = 0; t < 4; t++) { bits[t] = or_default_bits[t]; vals[t] = or_default_vals[t]; }
     if (huff_optimal) {
-        /* mjpegenc.c ff_mjpeg_encode_stuffing -> mjpeg_build_optimal_huffman: the
-         * picture's symbols are buffered, counted, and the tables built before the
-         * header and the scan are written. */
         static uint32_t counts[4][256];
         int last_dc[3] = { 128, 128, 128 };
         memset(counts, 0, sizeof counts);
         for (size_t b = 0; b < nblocks; b++)
-            or_count_block(counts, coef + b * 64, (int)(b % 6), last[b], last_dc);
+            or_count_block(counts, coef + b * 64, L->b[b % bpm].n, last[b], last_dc);
         for (int t = 0; t < 4; t++) {
             or_huff_optimal(counts[t], obits[t], ovals[t]);
             bits[t] = obits[t];
             vals[t] = ovals[t];
         }
     }
-    size_t hdr = or_header_tables(w, h, qscale, sar_num, sar_den, com_itu601, 0, bits, vals, out, cap);
-    if (!hdr) { free(coef); free(last); return 0; }
+    int hs[3], vs3[3];
+    or_hvsample(cfmt, hs, vs3);
+    size_t pos = or_header_fmt(w, h, cfmt, qscale, sar_num, sar_den, com_itu601,
+                               rst ? (w - 1) / (8 * hs[0]) + 1 : 0, bits, vals, out, cap);
+    int ok = pos != 0;
 
     or_huff hf; or_huff_init_tables(&hf, bits, vals);
-    or_pb pb = { out + hdr, cap - hdr, 0, 0 };
+    or_pb seg = { segbuf, seg_cap, 0, 0 };
     int last_dc[3] = { 128, 128, 128 };
-    for (size_t b = 0; b < nblocks; b++)
-        or_encode_block(&pb, &hf, coef + b * 64, (int)(b % 6), last[b], last_dc);
-    free(coef); free(last);
-
-    int pad = (int)((8 - (pb.nbits & 7)) & 7);
-    if (pad) pb_put(&pb, pad, (1u << pad) - 1);
-    if (pb.overflow) return 0;
-    size_t size = pb.nbits >> 3;
-    uint8_t *buf = out + hdr;
-    size_t nff = 0;
-    for (size_t i = 0; i < size; i++) nff += (buf[i] == 0xFF);
-    if (hdr + size + nff + 2 > cap) return 0;
-    size_t ff = nff;
-    for (size_t i = size; i-- > 0 && ff;) {          /* in-place expansion, back to front */
-        uint8_t val = buf[i];
-        if (val == 0xFF) { buf[i + ff] = 0; ff--; }
-        buf[i + ff] = val;
+    const size_t row_blocks = (size_t)mcw * bpm;
+    for (size_t b = 0; ok && b < nblocks; b++) {
+        or_encode_block(&seg, &hf, coef + b * 64, L->b[b % bpm].n, last[b], last_dc);
+        if (rst && (b + 1) % row_blocks == 0 && b + 1 < nblocks) {
+            const int row = (int)(b / row_blocks);
+            ok = or_flush_segment(&seg, out, cap, &pos) == 0 && pos + 2 <= cap;
+            if (ok) { out[pos++] = 0xFF; out[pos++] = (uint8_t)(0xD0 + (row & 7)); }
+            last_dc[0] = last_dc[1] = last_dc[2] = 128;
+        }
     }
-    size_t total = hdr + size + nff;
-    out[total] = 0xFF; out[total + 1] = 0xD9;         /* EOI */
-    return total + 2;
+    if (ok) ok = or_flush_segment(&seg, out, cap, &pos) == 0 && pos + 2 <= cap;
+    free(coef); free(last); free(segbuf);
+    if (!ok) return 0;
+    out[pos++] = 0xFF; out[pos++] = 0xD9;             /* EOI */
+    return pos;
+}
+
+size_t or_encode_planes_ex(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                           int w, int h, int qscale, int sar_num, int sar_den, int com_itu601,
+                           int huff_optimal, uint8_t *out, size_t cap)
+{
+    return or_encode_planes_cfmt(y, ys, u, us, v, vs, w, h, 0, qscale, sar_num, sar_den, com_itu601,
+                                 huff_optimal, 0, out, cap);
 }
 
 size_t or_encode_planes(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
@@ -946,32 +1065,45 @@ int or_local_pos(int sub, int pos)
     return pos >> sub;
 }
 
-/* Full worker path for one yuv420p/yuvj420p frame: optional bicubic resize and
- * the auto-inserted tv->pc conversion (swscale context yuv420p -> yuvj420p), then
- * the mjpeg encode.  in_full_range: 1 for yuvj420p input (no conversion). */
+/* Full worker path for one frame of chroma format cfmt (yuv420p/422p/444p or their yuvj
+ * variants): optional bicubic resize and the auto-inserted tv->pc conversion (swscale
+ * context yuv4xxp -> yuvj4xxp), then the mjpeg encode.  in_full_range: 1 for yuvj input
+ * (no conversion).  Chroma siting per direction: get_local_pos(shift, -513). */
+size_t or_encode_frame_cfmt(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
+                            int sw, int sh, int dw, int dh, int cfmt, int in_full_range, int qscale,
+                            int sar_num, int sar_den, int bitexact_sws, int huff_optimal, int rst,
+                            uint8_t *out, size_t cap)
+{
+    if (cfmt < 0 || cfmt > 2) return 0;
+    int need_sws = (sw != dw || sh != dh || !in_full_range);
+    if (!need_sws)
+        return or_encode_planes_cfmt(y, ys, u, us, v, vs, sw, sh, cfmt, qscale, sar_num, sar_den, 0,
+                                     huff_optimal, rst, out, cap);
+    const int hsh = or_layouts[cfmt].hshift, vsh = or_layouts[cfmt].vshift;
+    int dcw = (dw + hsh) >> hsh, dch = (dh + vsh) >> vsh, scw = (sw + hsh) >> hsh, sch = (sh + vsh) >> vsh;
+    uint8_t *Y = (uint8_t *)malloc((size_t)dw * dh);
+    uint8_t *U = (uint8_t *)malloc((size_t)dcw * dch);
+    uint8_t *V = (uint8_t *)malloc((size_t)dcw * dch);
+    int rl = in_full_range ? 0 : 1, rc = in_full_range ? 0 : 2;
+    int lp = or_local_pos(0, 0), cph = or_local_pos(hsh, -513), cpv = or_local_pos(vsh, -513);
+    size_t n = 0;
+    if (Y && U && V &&
+        !or_scale_plane(y, ys, sw, sh, Y, dw, dw, dh, rl, bitexact_sws, lp, lp, lp, lp) &&
+        !or_scale_plane(u, us, scw, sch, U, dcw, dcw, dch, rc, bitexact_sws, cph, cph, cpv, cpv) &&
+        !or_scale_plane(v, vs, scw, sch, V, dcw, dcw, dch, rc, bitexact_sws, cph, cph, cpv, cpv))
+        n = or_encode_planes_cfmt(Y, dw, U, dcw, V, dcw, dw, dh, cfmt, qscale, sar_num, sar_den, 0,
+                                  huff_optimal, rst, out, cap);
+    free(Y); free(U); free(V);
+    return n;
+}
+
 size_t or_encode_frame_ex(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,
                           int sw, int sh, int dw, int dh, int in_full_range, int qscale,
                           int sar_num, int sar_den, int bitexact_sws, int huff_optimal,
                           uint8_t *out, size_t cap)
 {
-    int need_sws = (sw != dw || sh != dh || !in_full_range);
-    if (!need_sws)
-        return or_encode_planes_ex(y, ys, u, us, v, vs, sw, sh, qscale, sar_num, sar_den, 0, huff_optimal,
-                                   out, cap);
-    int dcw = (dw + 1) >> 1, dch = (dh + 1) >> 1, scw = (sw + 1) >> 1, sch = (sh + 1) >> 1;
-    uint8_t *Y = (uint8_t *)malloc((size_t)dw * dh);
-    uint8_t *U = (uint8_t *)malloc((size_t)dcw * dch);
-    uint8_t *V = (uint8_t *)malloc((size_t)dcw * dch);
-    int rl = in_full_range ? 0 : 1, rc = in_full_range ? 0 : 2;
-    int lp = or_local_pos(0, 0), cp = or_local_pos(1, -513);
-    size_t n = 0;
-    if (!or_scale_plane(y, ys, sw, sh, Y, dw, dw, dh, rl, bitexact_sws, lp, lp, lp, lp) &&
-        !or_scale_plane(u, us, scw, sch, U, dcw, dcw, dch, rc, bitexact_sws, cp, cp, cp, cp) &&
-        !or_scale_plane(v, vs, scw, sch, V, dcw, dcw, dch, rc, bitexact_sws, cp, cp, cp, cp))
-        n = or_encode_planes_ex(Y, dw, U, dcw, V, dcw, dw, dh, qscale, sar_num, sar_den, 0, huff_optimal,
-                                out, cap);
-    free(Y); free(U); free(V);
-    return n;
+    return or_encode_frame_cfmt(y, ys, u, us, v, vs, sw, sh, dw, dh, 0, in_full_range, qscale, sar_num,
+                                sar_den, bitexact_sws, huff_optimal, 0, out, cap);
 }
 
 size_t or_encode_frame(const uint8_t *y, int ys, const uint8_t *u, int us, const uint8_t *v, int vs,

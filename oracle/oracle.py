@@ -54,6 +54,15 @@ def lib():
         L.or_encode_frame_ex.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, C.c_int] + [C.c_int] * 10 + \
             [u8p, C.c_size_t]
         L.or_encode_frame_ex.restype = C.c_size_t
+        L.or_header_cfmt.argtypes = [C.c_int] * 8 + [u8p, C.c_size_t]
+        L.or_header_cfmt.restype = C.c_size_t
+        L.or_frame_coeffs_cfmt.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, C.c_int] + [C.c_int] * 4 + \
+            [C.POINTER(C.c_int16), C.POINTER(C.c_int8)]
+        L.or_mcu_grid.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.or_mcu_grid.restype = None
+        L.or_encode_frame_cfmt.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, C.c_int] + [C.c_int] * 12 + \
+            [u8p, C.c_size_t]
+        L.or_encode_frame_cfmt.restype = C.c_size_t
         L.or_huff_optimal.argtypes = [C.POINTER(C.c_uint32), u8p, u8p]
         L.or_huff_optimal.restype = C.c_int
         _lib = L
@@ -96,13 +105,39 @@ def huff_table(table_id: int):
     return size, code
 
 
-def header(width, height, qscale, sar=(1, 1), com_itu601=False, dri=0) -> bytes:
+CHROMA_FORMATS = {"420": 0, "422": 1, "444": 2}
+
+
+def _cfmt(chroma) -> int:
+    return CHROMA_FORMATS[str(chroma)] if not isinstance(chroma, int) else int(chroma)
+
+
+def header(width, height, qscale, sar=(1, 1), com_itu601=False, dri=0, chroma="420",
+           rst=False) -> bytes:
+    """Per-config header.  dri: an explicit DRI interval (4:2:0 only); rst: the DRI slice
+    threading writes for `chroma` (MCUs per MCU row)."""
     buf = np.zeros(4096, np.uint8)
-    n = lib().or_header(int(width), int(height), int(qscale), int(sar[0]), int(sar[1]),
-                        int(bool(com_itu601)), int(dri), _p(buf, C.c_uint8), buf.size)
+    if dri:
+        n = lib().or_header(int(width), int(height), int(qscale), int(sar[0]), int(sar[1]),
+                            int(bool(com_itu601)), int(dri), _p(buf, C.c_uint8), buf.size)
+    else:
+        n = lib().or_header_cfmt(int(width), int(height), _cfmt(chroma), int(qscale), int(sar[0]),
+                                 int(sar[1]), int(bool(com_itu601)), int(bool(rst)),
+                                 _p(buf, C.c_uint8), buf.size)
     if n == 0:
         raise RuntimeError("or_header failed")
     return buf[:n].tobytes()
+
+
+def mcu_grid(width, height, chroma="420"):
+    """(MCUs per row, MCU rows) of a frame."""
+    a, b = C.c_int(), C.c_int()
+    lib().or_mcu_grid(_cfmt(chroma), int(width), int(height), C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def blocks_per_mcu(chroma="420") -> int:
+    return (6, 8, 6)[_cfmt(chroma)]
 
 
 def _planes(y, u, v):
@@ -112,21 +147,22 @@ def _planes(y, u, v):
     return y, u, v
 
 
-def frame_coeffs(y, u, v, qscale):
-    """Quantized coefficients (natural order) of every block in MCU order + last index."""
+def frame_coeffs(y, u, v, qscale, chroma="420"):
+    """Quantized coefficients (natural order) of every block in coding order + last index."""
     y, u, v = _planes(y, u, v)
     h, w = y.shape
-    nblk = ((w + 15) // 16) * ((h + 15) // 16) * 6
+    mcw, mch = mcu_grid(w, h, chroma)
+    nblk = mcw * mch * blocks_per_mcu(chroma)
     coef = np.zeros((nblk, 64), np.int16)
     last = np.zeros(nblk, np.int8)
-    lib().or_frame_coeffs(_p(y, C.c_uint8), y.strides[0], _p(u, C.c_uint8), u.strides[0],
-                          _p(v, C.c_uint8), v.strides[0], w, h, int(qscale),
-                          _p(coef, C.c_int16), _p(last, C.c_int8))
+    lib().or_frame_coeffs_cfmt(_p(y, C.c_uint8), y.strides[0], _p(u, C.c_uint8), u.strides[0],
+                               _p(v, C.c_uint8), v.strides[0], w, h, _cfmt(chroma), int(qscale),
+                               _p(coef, C.c_int16), _p(last, C.c_int8))
     return coef, last
 
 
 def _cap(w, h):
-    return 4096 + ((w + 15) // 16) * ((h + 15) // 16) * 6 * 420 + 64
+    return 4096 + ((w + 15) // 16) * ((h + 15) // 16) * 12 * 420 + 64
 
 
 def encode_planes(y, u, v, qscale, sar=(1, 1), com_itu601=False) -> bytes:
@@ -172,9 +208,11 @@ def scale_plane(src, dst_w, dst_h, range_mode=0, bitexact=True, chroma=False):
 
 
 def encode_frame(y, u, v, dst_w=None, dst_h=None, full_range=False, qscale=5, sar=(1, 1),
-                 bitexact_sws=True, huffman="default") -> bytes:
+                 bitexact_sws=True, huffman="default", chroma="420", rst=False) -> bytes:
     """Whole worker path for one frame: [bicubic resize] + tv->pc + mjpeg encode with
-    -huffman default (Annex K tables) or optimal (per-frame tables, mjpegenc_huffman.c)."""
+    -huffman default (Annex K tables) or optimal (per-frame tables, mjpegenc_huffman.c),
+    chroma format 420/422/444, and rst=True for the slice-threaded layout (DRI, one
+    restart interval per MCU row)."""
     if huffman not in ("default", "optimal"):
         raise ValueError(huffman)
     y, u, v = _planes(y, u, v)
@@ -182,13 +220,13 @@ def encode_frame(y, u, v, dst_w=None, dst_h=None, full_range=False, qscale=5, sa
     dw = sw if dst_w is None else dst_w
     dh = sh if dst_h is None else dst_h
     out = np.zeros(_cap(dw, dh), np.uint8)
-    n = lib().or_encode_frame_ex(_p(y, C.c_uint8), y.strides[0], _p(u, C.c_uint8), u.strides[0],
-                                 _p(v, C.c_uint8), v.strides[0], sw, sh, dw, dh,
-                                 int(bool(full_range)), int(qscale), int(sar[0]), int(sar[1]),
-                                 int(bool(bitexact_sws)), int(huffman == "optimal"),
-                                 _p(out, C.c_uint8), out.size)
+    n = lib().or_encode_frame_cfmt(_p(y, C.c_uint8), y.strides[0], _p(u, C.c_uint8), u.strides[0],
+                                   _p(v, C.c_uint8), v.strides[0], sw, sh, dw, dh, _cfmt(chroma),
+                                   int(bool(full_range)), int(qscale), int(sar[0]), int(sar[1]),
+                                   int(bool(bitexact_sws)), int(huffman == "optimal"), int(bool(rst)),
+                                   _p(out, C.c_uint8), out.size)
     if n == 0:
-        raise RuntimeError("or_encode_frame_ex failed")
+        raise RuntimeError("or_encode_frame_cfmt failed")
     return out[:n].tobytes()
 
 

@@ -9,22 +9,23 @@ import numpy as np
 import pytest
 
 import oracle
-from ffmpeg_distributed_amd.encoder import MjpegEncoder, split_i420, pack_i420, i420_frame_bytes
+from ffmpeg_distributed_amd.encoder import (MjpegEncoder, split_i420, pack_i420, i420_frame_bytes,
+                                            chroma_size)
 from ffmpeg_distributed_amd.testsrc import testsrc2_i420 as make_testsrc
 
 pytestmark = pytest.mark.gpu
 
 
-def rand_frames(w, h, n, seed, kind="noise"):
+def rand_frames(w, h, n, seed, kind="noise", chroma="420"):
     rng = np.random.default_rng(seed)
-    fb = i420_frame_bytes(w, h)
+    fb = i420_frame_bytes(w, h, chroma)
+    cw, ch = chroma_size(w, h, chroma)
     if kind == "noise":
         return rng.integers(0, 256, (n, fb), dtype=np.uint8)
     if kind == "smooth":
         out = []
         for i in range(n):
             yy, xx = np.mgrid[0:h, 0:w]
-            cw, ch = (w + 1) // 2, (h + 1) // 2
             cy, cx = np.mgrid[0:ch, 0:cw]
             y = (128 + 90 * np.sin(xx / (5 + i) + yy / 9) + rng.normal(0, 3, (h, w))).clip(0, 255)
             u = (128 + 50 * np.cos(cx / 4 + i)).clip(0, 255) + 0 * cy
@@ -38,23 +39,31 @@ def rand_frames(w, h, n, seed, kind="noise"):
         for i in range(n):
             yy, xx = np.mgrid[0:h, 0:w]
             y = np.where(((xx + yy + i) & 1) == 0, 255, 0).astype(np.uint8)
-            cw, ch = (w + 1) // 2, (h + 1) // 2
             cy, cx = np.mgrid[0:ch, 0:cw]
             u = np.where(((cx // 2 + cy // 2) & 1) == 0, 255, 0).astype(np.uint8)
             v = (255 - u).astype(np.uint8)
             out.append(pack_i420(y, u, v))
         return np.stack(out)
     if kind == "testsrc":
-        return np.stack([make_testsrc(w, h, seed + i) for i in range(n)])
+        out = []
+        for i in range(n):
+            y, u, v = split_i420(make_testsrc(w, h, seed + i), w, h)
+            if chroma != "420":  # the 4:2:0 chroma, replicated to the format's plane size
+                rr = 1 if chroma == "422" else 2
+                u = np.repeat(np.repeat(u, 2, 0), rr, 1)[:ch, :cw]
+                v = np.repeat(np.repeat(v, 2, 0), rr, 1)[:ch, :cw]
+            out.append(pack_i420(y, u, v))
+        return np.stack(out)
     raise ValueError(kind)
 
 
-def oracle_frames(frames, w, h, q, full_range, dw=None, dh=None, sar=(1, 1), huffman="default"):
+def oracle_frames(frames, w, h, q, full_range, dw=None, dh=None, sar=(1, 1), huffman="default",
+                  chroma="420", rst=False):
     out = []
     for f in frames:
-        y, u, v = split_i420(f, w, h)
+        y, u, v = split_i420(f, w, h, chroma)
         out.append(oracle.encode_frame(y, u, v, dst_w=dw, dst_h=dh, full_range=full_range,
-                                       qscale=q, sar=sar, huffman=huffman))
+                                       qscale=q, sar=sar, huffman=huffman, chroma=chroma, rst=rst))
     return out
 
 
@@ -210,3 +219,90 @@ def test_4k_full_size_properties():
         assert im.size == (w, h)
     y, u, v = split_i420(frames[0], w, h)
     assert a[0] == oracle.encode_frame(y, u, v, qscale=5)
+
+
+# ------------------------------------------------ 4:2:2 / 4:4:4 and the RST layout (§8f row 4)
+FMT_CASES = [
+    # (w, h, q, full_range, kind, chroma)
+    (72, 40, 5, False, "smooth", "422"),
+    (72, 40, 5, False, "smooth", "444"),
+    (101, 57, 3, True, "noise", "422"),
+    (101, 57, 3, True, "noise", "444"),
+    (130, 66, 4, False, "checker", "444"),
+    (16, 16, 5, True, "flat", "422"),
+    (8, 8, 3, False, "smooth", "444"),
+    (9, 17, 2, True, "noise", "444"),
+    (1920, 1080, 5, False, "testsrc", "422"),
+    (1280, 720, 3, True, "testsrc", "444"),
+]
+
+
+@pytest.mark.parametrize("w,h,q,full,kind,chroma", FMT_CASES)
+def test_chroma_formats_match_oracle(w, h, q, full, kind, chroma):
+    n = 3
+    frames = rand_frames(w, h, n, seed=w * 7 + h + q, kind=kind, chroma=chroma)
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=2, chroma=chroma) as enc:
+        got = enc.encode(frames)
+    ref = oracle_frames(frames, w, h, q, full, chroma=chroma)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+@pytest.mark.parametrize("w,h,q,full,kind,chroma", [c + ("420",) for c in CASES] + FMT_CASES)
+def test_rst_layout_matches_oracle(w, h, q, full, kind, chroma):
+    """Slice-threaded layout: DRI, one entropy-coded segment per MCU row, RST0..7."""
+    n = 3
+    frames = rand_frames(w, h, n, seed=w * 5 + h + q, kind=kind, chroma=chroma)
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=3, chroma=chroma, rst=True) as enc:
+        got = enc.encode(frames)
+    ref = oracle_frames(frames, w, h, q, full, chroma=chroma, rst=True)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+@pytest.mark.parametrize("chroma", ["422", "444"])
+def test_coefficients_match_oracle_422_444(chroma):
+    w, h, q = 101, 57, 4
+    frames = rand_frames(w, h, 2, seed=3, kind="smooth", chroma=chroma)
+    with MjpegEncoder(0, w, h, qscale=q, full_range=True, max_batch=2, debug_coefs=True,
+                      chroma=chroma, rst=True) as enc:
+        enc.submit(frames)
+        enc.sync()
+        for i in range(2):
+            y, u, v = split_i420(frames[i], w, h, chroma)
+            ref, _ = oracle.frame_coeffs(y, u, v, q, chroma)
+            got = enc.debug_coefs(i)
+            bad = np.nonzero((got != ref).any(1))[0]
+            assert bad.size == 0, (i, bad[:10])
+
+
+@pytest.mark.parametrize("chroma,rst", [("422", False), ("444", True), ("420", True)])
+def test_scale_422_444_rst_matches_oracle(chroma, rst):
+    sw, sh, dw, dh, q = 160, 96, 80, 48, 3
+    frames = rand_frames(sw, sh, 3, seed=13, kind="smooth", chroma=chroma)
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, max_batch=2, chroma=chroma, rst=rst) as enc:
+        got = enc.encode(frames)
+    assert got == oracle_frames(frames, sw, sh, q, False, dw, dh, chroma=chroma, rst=rst)
+
+
+def test_rst_4k_full_size():
+    """4K with RST (135 restart intervals per frame, 23 chunks per row): equal to the
+    oracle on frame 0, decodable, same pixels as the plain layout."""
+    from PIL import Image
+    w, h = 3840, 2160
+    frames = np.stack([make_testsrc(w, h, t) for t in range(3)])
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=3, rst=True) as enc:
+        a = enc.encode(frames)
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=3) as enc:
+        b = enc.encode(frames)
+    y, u, v = split_i420(frames[0], w, h)
+    assert a[0] == oracle.encode_frame(y, u, v, qscale=5, rst=True)
+    for ja, jb in zip(a, b):
+        ia, ib = Image.open(io.BytesIO(ja)), Image.open(io.BytesIO(jb))
+        assert np.array_equal(np.asarray(ia), np.asarray(ib))
+
+
+def test_rst_with_optimal_is_rejected():
+    from ffmpeg_distributed_amd._lib import MjgError
+    with pytest.raises(MjgError):
+        MjpegEncoder(0, 64, 64, huffman="optimal", rst=True)

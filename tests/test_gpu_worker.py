@@ -90,3 +90,31 @@ def test_worker_huffman_optimal(huffman, monkeypatch):
         y, u, v = split_i420(f, w, h)
         ref = oracle.encode_frame(y, u, v, full_range=False, qscale=q, sar=(1, 1), huffman="optimal")
         assert packets[i] == ref, f"frame {i}"
+
+
+@pytest.mark.parametrize("fourcc,chroma,extra", [
+    (b"Y42B", "422", ["-slices", "4"]),                       # 4:2:2 + RST layout
+    (b"444P", "444", ["-thread_type", "slice", "-pix_fmt", "yuvj444p"]),
+    (b"I420", "420", ["-threads", "1", "-slices", "2", "-huffman", "optimal"]),  # slices force default
+])
+def test_worker_raw_mkv_422_444_rst(fourcc, chroma, extra, monkeypatch):
+    """Raw 4:2:2 / 4:4:4 Matroska segments and slice-threaded remote_args:
+    the worker keeps the input sampling and writes the RST layout."""
+    from ffmpeg_distributed_amd.encoder import i420_frame_bytes
+    w, h, n, q = 112, 72, 5, 4
+    fb = i420_frame_bytes(w, h, chroma)
+    rng = np.random.default_rng(4)
+    frames = [np.clip(rng.normal(128, 40, fb), 0, 255).astype(np.uint8) for _ in range(n)]
+    buf = io.BytesIO()
+    wr = container.MkvWriter(buf, w, h, Fraction(25), codec="V_UNCOMPRESSED", colour_space=fourcc,
+                             colour_range=1)
+    for f in frames:
+        wr.write_frame(f.tobytes())
+    wr.close()
+    args = [x.format(q=q) for x in ARGS[:6]] + ["-bitexact"] + extra
+    r, packets, _ = _run(buf.getvalue(), args, monkeypatch, 2)
+    assert len(packets) == n
+    for i, f in enumerate(frames):
+        y, u, v = split_i420(f, w, h, chroma)
+        ref = oracle.encode_frame(y, u, v, full_range=False, qscale=q, sar=(1, 1), chroma=chroma, rst=True)
+        assert packets[i] == ref, f"frame {i}"

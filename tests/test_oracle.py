@@ -272,3 +272,133 @@ def test_oracle_scaled_frame_decodes():
 def test_pack_split_roundtrip():
     fr = make_testsrc(101, 57, 2)
     assert (pack_i420(*split_i420(fr, 101, 57)) == fr).all()
+
+
+# ------------------------------------------------ 4:2:2 / 4:4:4 and the RST layout
+SHIFTS = {"420": (1, 1), "422": (1, 0), "444": (0, 0)}
+
+
+def smooth_planes(w, h, chroma, seed=0):
+    hs, vs = SHIFTS[chroma]
+    cw, ch = (w + hs) >> hs, (h + vs) >> vs
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    y = (128 + 80 * np.sin(xx / 6) * np.cos(yy / 9) + rng.normal(0, 2, (h, w))).clip(0, 255)
+    cy, cx = np.mgrid[0:ch, 0:cw]
+    u = (128 + 40 * np.sin(cx / 5) + 20 * np.cos(cy / 7)).clip(0, 255)
+    v = (128 + 40 * np.cos(cy / 4) - 15 * np.sin(cx / 3)).clip(0, 255)
+    return y.astype(np.uint8), u.astype(np.uint8), v.astype(np.uint8)
+
+
+@pytest.mark.parametrize("chroma,sof", [("420", (0x22, 0x11, 0x11)), ("422", (0x22, 0x12, 0x12)),
+                                        ("444", (0x12, 0x12, 0x12))])
+@pytest.mark.parametrize("rst", [False, True])
+def test_header_sampling_and_dri(chroma, sof, rst):
+    """SOF0 factors follow ff_mjpeg_init_hvsample (4:4:4 is 1x2 for every component); DRI
+    (slice threading) sits between DQT and DHT with interval = MCUs per MCU row."""
+    w, h = 101, 57
+    segs = segments(oracle.header(w, h, 5, chroma=chroma, rst=rst) + b"\xff\xd9")
+    markers = [m for m, _ in segs]
+    assert markers == [0xE0, 0xDB] + ([0xDD] if rst else []) + [0xC4, 0xC0, 0xDA, "scan"]
+    d = dict(segs[:-1])
+    assert d[0xC0][6:] == bytes([1, sof[0], 0, 2, sof[1], 0, 3, sof[2], 0])
+    if rst:
+        mcw, _ = oracle.mcu_grid(w, h, chroma)
+        assert d[0xDD] == bytes([mcw >> 8, mcw & 255]) and mcw == -(-w // (8 if chroma == "444" else 16))
+    assert _lib.build_header(w, h, 5, (1, 1), chroma=chroma, rst=rst) == \
+        oracle.header(w, h, 5, chroma=chroma, rst=rst)
+
+
+def test_luma_blocks_do_not_depend_on_chroma_format():
+    """The luma blocks of a 4:2:2 frame are the 4:2:0 ones; 4:4:4 codes each 16x16 macroblock
+    as two 8x16 MCUs (left: Y TL, Y BL; right: Y TR, Y BR)."""
+    w, h = 48, 32
+    y, u, v = smooth_planes(w, h, "420", 1)
+    c420, _ = oracle.frame_coeffs(y, u, v, 4, "420")
+    y2, u2, v2 = smooth_planes(w, h, "422", 1)
+    c422, _ = oracle.frame_coeffs(y, u2, v2, 4, "422")
+    y4, u4, v4 = smooth_planes(w, h, "444", 1)
+    c444, _ = oracle.frame_coeffs(y, u4, v4, 4, "444")
+    lum420 = c420.reshape(-1, 6, 64)[:, :4]
+    np.testing.assert_array_equal(c422.reshape(-1, 8, 64)[:, :4], lum420)
+    l444 = c444.reshape(-1, 2, 6, 64)[:, :, :2]          # [MB, left/right MCU, Y top/bottom]
+    np.testing.assert_array_equal(l444[:, 0, 0], lum420[:, 0])
+    np.testing.assert_array_equal(l444[:, 0, 1], lum420[:, 2])
+    np.testing.assert_array_equal(l444[:, 1, 0], lum420[:, 1])
+    np.testing.assert_array_equal(l444[:, 1, 1], lum420[:, 3])
+    # chroma: 4:2:2 Cb top / Cb bottom of MCU 0 are the first two 8x8 blocks of the Cb column
+    assert c422[4, 0] == (int(u2[:8, :8].astype(int).sum()) + 32) // 64
+    assert c422[5, 0] == (int(u2[8:16, :8].astype(int).sum()) + 32) // 64
+    assert c422[6, 0] == (int(v2[:8, :8].astype(int).sum()) + 32) // 64
+
+
+@pytest.mark.parametrize("chroma", ["420", "422", "444"])
+@pytest.mark.parametrize("w,h", [(72, 40), (101, 57), (64, 48), (8, 8), (200, 130)])
+def test_chroma_formats_and_rst_decode(chroma, w, h):
+    """Each format decodes with libjpeg to the expected sampling at high PSNR; the RST
+    layout decodes to exactly the same pixels (same coefficients, rows as restart
+    intervals), carries RST0..7 cyclically after every MCU row but the last, and every
+    restart interval is byte aligned with its 0xFF bytes stuffed."""
+    y, u, v = smooth_planes(w, h, chroma, 2)
+    plain = oracle.encode_frame(y, u, v, full_range=True, qscale=3, chroma=chroma)
+    rst = oracle.encode_frame(y, u, v, full_range=True, qscale=3, chroma=chroma, rst=True)
+    a, b = Image.open(io.BytesIO(plain)), Image.open(io.BytesIO(rst))
+    a.load()
+    b.load()
+    hv = {"420": ((2, 2), (1, 1)), "422": ((2, 2), (1, 2)), "444": ((1, 2), (1, 2))}[chroma]
+    assert a.layer == [(1, *hv[0], 0), (2, *hv[1], 0), (3, *hv[1], 0)]
+    np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    got = np.asarray(a.convert("YCbCr"))[..., 0].astype(float)
+    assert 10 * np.log10(255 ** 2 / np.mean((got - y) ** 2)) > 30
+    _, mch = oracle.mcu_grid(w, h, chroma)
+    scan = segments(rst)[-1][1]
+    marks = [scan[i + 1] for i in range(len(scan) - 1) if scan[i] == 0xFF and scan[i + 1] != 0]
+    assert marks == [0xD0 + (r & 7) for r in range(mch - 1)]
+    if mch == 1:
+        assert rst == plain                      # one MCU row: no DRI, no RST
+
+
+def test_rst_restarts_dc_prediction():
+    """A flat frame: every MCU row after the first restarts its DC predictors at 128, so with
+    RST every row codes the same bits (plain mode codes DC differences of 0 after row 0)."""
+    w, h = 64, 64
+    y = np.full((h, w), 200, np.uint8)
+    u = np.full((h // 2, w // 2), 90, np.uint8)
+    j = oracle.encode_frame(y, u, u.copy(), full_range=True, qscale=5, rst=True)
+    scan = segments(j)[-1][1]
+    rows, cur = [], bytearray()
+    i = 0
+    while i < len(scan):
+        if scan[i] == 0xFF and 0xD0 <= scan[i + 1] <= 0xD7:
+            rows.append(bytes(cur))
+            cur = bytearray()
+            i += 2
+            continue
+        cur.append(scan[i])
+        i += 1
+    rows.append(bytes(cur))
+    assert len(rows) == 4 and len(set(rows)) == 1
+
+
+def test_rst_and_optimal_are_exclusive():
+    y, u, v = smooth_planes(32, 32, "420")
+    with pytest.raises(RuntimeError):
+        oracle.encode_frame(y, u, v, full_range=True, huffman="optimal", rst=True)
+
+
+@pytest.mark.parametrize("chroma", ["422", "444"])
+def test_tv_range_and_scale_for_422_444(chroma):
+    """yuv422p/yuv444p (tv) input: swscale's per-plane path with the format's chroma plane
+    sizes and siting; the frame decodes and scaled frames keep the sampling."""
+    w, h, dw, dh = 96, 64, 48, 40
+    y, u, v = smooth_planes(w, h, chroma, 5)
+    j = oracle.encode_frame(y, u, v, dst_w=dw, dst_h=dh, full_range=False, qscale=3, chroma=chroma)
+    im = Image.open(io.BytesIO(j))
+    im.load()
+    assert im.size == (dw, dh)
+    j2 = oracle.encode_frame(y, u, v, full_range=False, qscale=3, chroma=chroma)
+    im2 = Image.open(io.BytesIO(j2))
+    im2.load()
+    got = np.asarray(im2.convert("YCbCr"))[..., 0].astype(float)
+    ref = np.clip((y.astype(float) - 16) * 255 / 219, 0, 255)     # tv -> pc luma
+    assert 10 * np.log10(255 ** 2 / np.mean((got - ref) ** 2)) > 30

@@ -38,6 +38,30 @@ def test_profile_huffman_modes(args, huff):
     assert profile.parse(args).huffman == huff
 
 
+@pytest.mark.parametrize("extra,rst", [
+    ("", False),                                   # default: frame threading, no DRI/RST
+    ("-threads 8", False),
+    ("-slices 1", False),
+    ("-slices 4", True),                           # slice_context_count = -slices
+    ("-threads 1 -slices 2", True),
+    ("-thread_type slice", True),                  # -threads auto (> 1) slice threads
+    ("-thread_type slice -threads 4", True),
+    ("-thread_type slice -threads 1", False),
+    ("-thread_type slice+frame -threads 4", False),  # frame threading wins for encoders
+    ("-thread_type frame", False),
+])
+def test_profile_slice_threading(extra, rst):
+    p = profile.parse("-c:v mjpeg -q:v 5 -dct int -bitexact " + extra)
+    assert p.rst == rst
+    assert p.huffman == ("default" if rst else "optimal")   # slices force default tables
+
+
+@pytest.mark.parametrize("pf,chroma", [("yuvj420p", "420"), ("yuvj422p", "422"), ("yuvj444p", "444")])
+def test_profile_pix_fmt(pf, chroma):
+    assert profile.parse(f"-c:v mjpeg -q:v 5 -dct int -bitexact -pix_fmt {pf}").chroma == chroma
+    assert profile.parse("-c:v mjpeg -q:v 5 -dct int -bitexact").chroma is None
+
+
 @pytest.mark.parametrize("q,expect", [(1, 2), (2, 2), (3, 3), (5, 5), (31, 31), (40, 31), (4.5, 5), (4.4, 4), (7.9, 8)])
 def test_profile_qscale_mapping(q, expect):
     # update_qscale: lambda = q*118 (truncated), qscale = (lambda*139 + 8192) >> 14
@@ -53,7 +77,9 @@ def test_profile_qscale_mapping(q, expect):
     "-vf scale=1920:-2 -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
     "-vf scale=1280:720:flags=lanczos -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
     "-vf scale=1280:720,hflip -c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
-    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -pix_fmt yuvj422p",
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -pix_fmt gray",
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -thread_type auto",
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -slices many",
 ])
 def test_profile_rejects_outside_gpu_path(args):
     prof, why = profile.try_parse(args)
@@ -121,9 +147,39 @@ def test_y4m_reader():
     np.testing.assert_array_equal(buf[:5], fr)
 
 
-def test_y4m_rejects_non_420():
-    with pytest.raises(ValueError):
-        container.Y4MReader(io.BytesIO(b"YUV4MPEG2 W16 H16 F25:1 C444\n"))
+def test_y4m_rejects_unsupported_sampling():
+    for c in (b"C411", b"Cmono", b"C444alpha", b"C420p10"):
+        with pytest.raises(ValueError):
+            container.Y4MReader(io.BytesIO(b"YUV4MPEG2 W16 H16 F25:1 " + c + b"\n"))
+
+
+@pytest.mark.parametrize("tag,chroma,cw,ch", [(b"C422", "422", 35, 38), (b"C444", "444", 70, 38),
+                                              (b"C420paldv", "420", 35, 19)])
+def test_y4m_reader_422_444(tag, chroma, cw, ch):
+    w, h = 70, 38
+    rng = np.random.default_rng(1)
+    fb = w * h + 2 * cw * ch
+    fr = rng.integers(0, 256, (3, fb), dtype=np.uint8)
+    rd = container.Y4MReader(io.BytesIO(_y4m(fr, w, h, extra=" Ip A1:1 " + tag.decode())))
+    assert rd.info.chroma == chroma and rd.info.frame_bytes == fb
+    buf = np.zeros((3, fb), np.uint8)
+    assert rd.read_into(buf, 3) == 3
+    np.testing.assert_array_equal(buf, fr)
+    # the writer's header reads back to the same stream description
+    hdr = container.y4m_header(rd.info)
+    assert container.Y4MReader(io.BytesIO(hdr)).info == rd.info
+
+
+@pytest.mark.parametrize("fourcc,chroma", [(b"Y42B", "422"), (b"444P", "444")])
+def test_source_reads_uncompressed_mkv_422_444(fourcc, chroma):
+    w, h = 48, 32
+    fb = container.StreamInfo(w, h, chroma=chroma).frame_bytes
+    fr = np.random.default_rng(2).integers(0, 256, (5, fb), dtype=np.uint8)
+    src = worker.Source(io.BytesIO(_mkv_raw(fr, w, h, colour=fourcc)))
+    assert src.child is None and src.info.chroma == chroma and src.info.frame_bytes == fb
+    buf = np.zeros((8, fb), np.uint8)
+    assert src.read_into(buf, 8) == 5
+    np.testing.assert_array_equal(buf[:5], fr)
 
 
 def _mkv_raw(frames, w, h, codec="V_UNCOMPRESSED", colour=b"I420", rng=1):
@@ -193,6 +249,32 @@ def test_worker_passthrough_runs_reference_command(tmp_path):
     calls = [json.loads(l) for l in open(log)]
     assert calls == [{"prog": "ffmpeg", "argv": worker.reference_argv(args)[1:], "host": "localhost"}]
     assert b"running ffmpeg on the CPU" in p.stderr
+
+
+def test_worker_pix_fmt_resample_falls_through_to_ffmpeg(tmp_path):
+    """-pix_fmt asking for another chroma sampling than the input's is not on the GPU path:
+    the frames read so far (and the rest) go to the real ffmpeg as y4m, with the
+    remote_args unchanged."""
+    log = tmp_path / "shim.log"
+    env = dict(os.environ, PATH=os.path.join(HERE, "shims") + os.pathsep + os.environ["PATH"],
+               SHIM_LOG=str(log), PYTHONPATH=ROOT)
+    w, h = 16, 8
+    fr = np.full((3, w * h + 2 * 8 * 4), 0x41, np.uint8)      # ASCII-safe: the shim reads text
+    fr[:, :7] = np.arange(3)[:, None] + 0x30
+    data = _y4m(fr, w, h, extra=" Ip A1:1 C420jpeg")
+    args = ["-c:v", "mjpeg", "-q:v", "5", "-dct", "int", "-bitexact", "-pix_fmt", "yuvj444p"]
+    p = subprocess.run([sys.executable, "-m", "ffmpeg_distributed_amd.worker", "--device", "0", *args],
+                       input=data, capture_output=True, env=env, timeout=60)
+    assert p.returncode == 0, p.stderr
+    calls = [json.loads(l) for l in open(log)]
+    assert calls == [{"prog": "ffmpeg", "argv": ["-f", "yuv4mpegpipe", "-i", "pipe:", *args, "-f",
+                                                 "matroska", "pipe:"], "host": "localhost"}]
+    body = p.stdout[len(b"ENC["):-1]
+    rd = container.Y4MReader(io.BytesIO(body))
+    assert (rd.info.width, rd.info.height, rd.info.chroma) == (w, h, "420")
+    buf = np.zeros_like(fr)
+    assert rd.read_into(buf, 3) == 3
+    np.testing.assert_array_equal(buf, fr)
 
 
 def test_progress_lines_parse_with_dispatcher_regex():
