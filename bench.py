@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     p.add_argument("--huffman", choices=["default", "optimal"], default=None)
+    p.add_argument("--rst", action="store_true",
+                   help="slice-threaded layout (-slices N: DRI + one restart interval per MCU row)")
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--pool", type=int, default=480, help="distinct resident frames per GPU")
@@ -151,8 +153,10 @@ def main():
                                                                      full_range=FULL)
     torch.cuda.synchronize()
 
+    if a.rst:
+        HUFF = "default"  # slice threading forces the default tables
     enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg, timing=True,
-                       huffman=HUFF)
+                       huffman=HUFF, rst=a.rst)
     bytes_out = []
 
     def step(s):
@@ -186,7 +190,7 @@ def main():
         with open(a.pmc) as f:
             pm = json.load(f)
         if pm.get("workload", {}).get("frames_per_launch") == seg and a.workload == "c2" and \
-                HUFF == "default":
+                HUFF == "default" and not a.rst:
             traffic = pm.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -217,7 +221,8 @@ def main():
                        "dst_height": DH, "qscale": Q, "frames_per_step": seg,
                        "global_batch": seg * world, "parallelism": f"segment-dp{world}",
                        "profile": (f"-vf scale={DW}:{DH}:flags=bicubic " if (DW, DH) != (W, H) else "")
-                       + f"-c:v mjpeg -q:v {Q} -dct int -huffman {HUFF} -bitexact"},
+                       + f"-c:v mjpeg -q:v {Q} -dct int -huffman {HUFF} -bitexact"
+                       + (" -slices 8" if a.rst else "")},
             "roofline": {"bound": "hbm", "kernel": "k_encode",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -606,8 +606,12 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_SCAN_BITS, 0);
-  k_scan_bits<<<nsegs, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits,
-                                             g.nchunks, c->d_work);
+  if (c->rst)
+    k_scan_bits_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits,
+                                                            g.nchunks, nsegs, c->d_work);
+  else
+    k_scan_bits<<<n, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, g.nchunks,
+                                           c->d_work);
   tmark(c, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, MJG_K_COUNT_FF, 0);
@@ -620,8 +624,8 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, MJG_K_SCAN_FF, 0);
   // optimal: header = default header - its 348 table values + the frame's
   if (c->rst) {  // segment sizes (each with its RSTn / EOI trailer), then per-frame offsets
-    k_scan_ff<<<nsegs, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_seg_size,
-                                             gpf, 0, nullptr, 0, nullptr);
+    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits,
+                                                          c->d_seg_size, gpf, nsegs);
     k_seg_sizes<<<n, 64, 0, c->stream>>>(c->d_seg_size, g.nseg, (int)c->hdr.size(), c->d_seg_off,
                                          c->d_frame_size);
   } else {

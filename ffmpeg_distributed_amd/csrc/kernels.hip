@@ -409,6 +409,11 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
 __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, int &chunk, int &bbase) {
   const int seg = t / g.nchunks;
   chunk = t - seg * g.nchunks;
+  if (g.nseg == 1) {  // one segment per frame (no RST): skip the second division
+    frame = seg;
+    bbase = 0;
+    return;
+  }
   frame = seg / g.nseg;
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
@@ -1125,6 +1130,33 @@ __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk
   if (threadIdx.x == 0) frame_bits[f] = t;
 }
 
+// RST mode: the same per segment with one wave per segment (a segment is one MCU row, a
+// few dozen chunks), 4 segments per 256-thread workgroup.
+__device__ __forceinline__ uint32_t wave_excl_scan_arr(const uint32_t *in, uint32_t *out, int n, int lane) {
+  uint32_t carry = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const uint32_t v = i < n ? in[i] : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (i < n) out[i] = carry + incl - v;
+    carry += __shfl(incl, 63, 64);
+  }
+  return carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ chunk_bits,
+                                                       uint32_t *__restrict__ chunk_off,
+                                                       uint32_t *__restrict__ seg_bits, int nchunks,
+                                                       int nsegs, uint32_t *__restrict__ work_ctr) {
+  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *work_ctr = 0;
+  if (sg >= nsegs) return;
+  uint32_t *cb = chunk_bits + (size_t)sg * nchunks;
+  for (int i = lane; i < nchunks; i += 64) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
+  const uint32_t t = wave_excl_scan_arr(cb, chunk_off + (size_t)sg * nchunks, nchunks, lane);
+  if (lane == 0) seg_bits[sg] = t;
+}
+
 // Word k (32 bits, MSB first) of frame f's unstuffed scan, for a word owned by chunk c
 // (its first bit lies in chunk c).  Bits past the chunk come from chunk c+1, or for the
 // frame's last chunk are the 1-bit padding to a byte boundary (ff_mjpeg_escape_FF pad).
@@ -1258,6 +1290,20 @@ __global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ g
     }
     frame_size[f] = (uint64_t)hl + ((frame_bits[f] + 7) >> 3) + t + 2;
   }
+}
+
+// RST mode, per segment (wave): scan of its groups' 0xFF counts -> stuffed segment size
+// including the 2-byte trailer (RSTn or, for the frame's last segment, EOI).
+__global__ __launch_bounds__(256) void k_scan_ff_seg(const uint32_t *__restrict__ group_ff,
+                                                     uint32_t *__restrict__ ff_off,
+                                                     const uint32_t *__restrict__ seg_bits,
+                                                     uint64_t *__restrict__ seg_size, int ngroups_per_seg,
+                                                     int nsegs) {
+  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (sg >= nsegs) return;
+  const size_t g0 = (size_t)sg * ngroups_per_seg;
+  const uint32_t t = wave_excl_scan_arr(group_ff + g0, ff_off + g0, ngroups_per_seg, lane);
+  if (lane == 0) seg_size[sg] = (uint64_t)((seg_bits[sg] + 7) >> 3) + t + 2;
 }
 
 // RST mode (one entropy-coded segment per MCU row): per frame, the segments' offsets after
