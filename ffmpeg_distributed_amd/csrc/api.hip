@@ -381,6 +381,43 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     const float b2 = (float)(B * B);
     memcpy(&tabs[608 + (i & 7) * 8 + ro], &b2, 4);
   }
+  // [680, 689): k_encode's column-skip limits for column pairs 1-3 (columns 2-7), three u16x2
+  // words per pair: Rmax, HI, LO.  A column's AC outputs all quantise to zero if
+  //   row 0:  |S| = |sum u_r| <= 16 T - 9          <= 8 max|u_r|, max|u_r| <= 2T - 2
+  //   row 4:  |S| = |sum +-u_r| <= 16 T - 9        <= 4 R  (the +-1 row sums to 0)
+  //   others: |S| <= T 2^17 - 2^16 - 1             <= L1(row) R / 2
+  // (T = ceil(5 2^18 / qmat) of that output, R = max - min of the column's row-pass values
+  // u_r, S the pass-2 sum before DESCALE; dct_quantize_c gives 0 iff |DESCALE(S)| < T).  With
+  // U = u + 32768 (the u16 image): skip iff R <= Rmax, max U <= HI, min U >= LO.
+  {
+    static const int kDot[64] = MJG_PASS2_DOT;
+    for (int jp = 1; jp < 4; jp++) {
+      uint32_t lim[3] = {0, 0, 0};
+      for (int h = 0; h < 2; h++) {
+        const int col = 2 * jp + h;
+        long long rmax = 65535, amax = 0;
+        for (int ro = 0; ro < 8; ro++) {
+          const long long qm = c->qmat[ro * 8 + col];
+          const long long T = ((5ll << 18) + qm - 1) / qm;
+          if (ro == 0) {
+            amax = std::max(0ll, 2 * T - 2);
+          } else if (ro == 4) {
+            rmax = std::min(rmax, 4 * T - 3);
+          } else {
+            long long l1 = 0;
+            for (int r = 0; r < 8; r++) l1 += std::abs(kDot[ro * 8 + r]);
+            rmax = std::min(rmax, (2 * (T * 131072 - 65536 - 1)) / l1);
+          }
+        }
+        rmax = std::max(0ll, rmax);
+        const long long hi = std::min(65535ll, 32768 + amax), lo = std::max(0ll, 32768 - amax);
+        lim[0] |= (uint32_t)rmax << (16 * h);
+        lim[1] |= (uint32_t)hi << (16 * h);
+        lim[2] |= (uint32_t)lo << (16 * h);
+      }
+      for (int i = 0; i < 3; i++) tabs[680 + 3 * (jp - 1) + i] = lim[i];
+    }
+  }
   // [672, 680): block-of-MCU descriptors in coding order (EncGeom): plane | chroma table << 2 |
   // dx8 << 3 | dy8 << 4 | DC predecessor distance << 8 (ff_mjpeg_encode_mb order; the
   // predecessor is the previous block of the same component)

@@ -42,7 +42,7 @@ constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 bl
 // fp32 exact-integer arithmetic (k_encode): adding kM = 1.5*2^23 rounds to an integer
 // (round-to-nearest-even) and keeps it in the low mantissa bits; kMb = kM + 32768 leaves
 // value + 32768 in the low 16 bits.  kRnd = 2^-10 turns floor(x/512 + 1/2) into RNE.
-constexpr int kTabWords = 680;  // device table block, see open_ctx
+constexpr int kTabWords = 692;  // device table block, see open_ctx
 constexpr float kM = 12582912.0f;
 constexpr float kMb = 12615680.0f;
 constexpr float kRnd = 0x1p-10f;
@@ -51,15 +51,16 @@ constexpr float kRnd = 0x1p-10f;
 // the 8 column inputs: the LLM butterfly's t/z terms multiplied out (rows 0/4: +-1 with
 // DESCALE 4; others: DESCALE 17).  kPass2Add: rounding constant minus 32768 * row sum
 // (the u16 row image carries +32768).
-__device__ static constexpr int kPass2Dot[64] = {
-    1, 1, 1, 1, 1, 1, 1, 1,
-    11363, 9633, 6437, 2260, -2260, -6437, -9633, -11363,
-    10703, 4433, -4433, -10703, -10703, -4433, 4433, 10703,
-    9633, -2259, -11362, -6436, 6436, 11362, 2259, -9633,
-    1, -1, -1, 1, 1, -1, -1, 1,
-    6437, -11362, 2261, 9633, -9633, -2261, 11362, -6437,
-    4433, -10704, 10704, -4433, -4433, 10704, -10704, 4433,
-    2260, -6436, 9633, -11363, 11363, -9633, 6436, -2260};
+#define MJG_PASS2_DOT                                                  \
+  {1, 1, 1, 1, 1, 1, 1, 1,                                             \
+   11363, 9633, 6437, 2260, -2260, -6437, -9633, -11363,               \
+   10703, 4433, -4433, -10703, -10703, -4433, 4433, 10703,             \
+   9633, -2259, -11362, -6436, 6436, 11362, 2259, -9633,               \
+   1, -1, -1, 1, 1, -1, -1, 1,                                         \
+   6437, -11362, 2261, 9633, -9633, -2261, 11362, -6437,               \
+   4433, -10704, 10704, -4433, -4433, 10704, -10704, 4433,             \
+   2260, -6436, 9633, -11363, 11363, -9633, 6436, -2260}
+__device__ static constexpr int kPass2Dot[64] = MJG_PASS2_DOT;
 // k_encode screen bit -> zigzag scan position.  Columns 0-3 (DC excluded) are shifted
 // into word A in the order col-major (col, row), columns 4-7 into word B, so the j-th
 // coefficient screened lands at bit 30-j (A) / 31-j (B).
@@ -115,6 +116,10 @@ __device__ __forceinline__ int range_chroma(int p) {
 }
 
 #define MJG_DESCALE(x, n) (((x) + (1 << ((n) - 1))) >> (n))
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 // One 8-point jfdctint butterfly on p[0], p[S], ... p[7S] (CONST_BITS 13, PASS1_BITS 4).
 // ROW: pass 1 (d0/d4 << 4, others descale 9); !ROW: pass 2 (descale 4 / 17).  Every
@@ -478,6 +483,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
   __shared__ uint8_t s_rc[MJG_RC_LUT ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
+  __shared__ uint32_t s_skip[12];                  // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   // per wave: the current frame's histogram (kCount) or code tables (kEmitFrame)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
@@ -496,6 +502,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_m2[64 + tid] = kPass2Add[tid];
     s_desc[tid] = tabs[672 + tid];
   }
+  if (tid < 12) s_skip[tid] = tabs[680 + tid];
   if (MJG_RC_LUT && RC)
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
@@ -665,10 +672,39 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
         uint32_t w[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
+        // Column skip (pairs 1-3): every AC output of a column quantises to zero when the
+        // column's row-pass values are small enough.  Rows 1-7 of pass 2 have coefficient
+        // sums 0, so |S_k| <= L1(row k) * R / 2 with R = max - min of the column; row 0 is
+        // the plain sum, |S_0| <= 8 max|u|.  open_ctx turns the quantiser thresholds into
+        // limits on R, max and min (u16 with the +32768 bias), tested with packed u16
+        // max/min and saturating subtracts; a column is skipped when every block of the
+        // chunk passes (wave ballot), its 8 screen bits are then 0.
+        bool skip0 = false, skip1 = false;
+        if (jp > 0) {
+          u16x2 mx = as_u16x2(w[0]), mn = mx;
+#pragma unroll
+          for (int r = 1; r < 8; r++) {
+            mx = __builtin_elementwise_max(mx, as_u16x2(w[r]));
+            mn = __builtin_elementwise_min(mn, as_u16x2(w[r]));
+          }
+          const uint32_t t =
+              as_u32(__builtin_elementwise_sub_sat(mx - mn, as_u16x2(s_skip[3 * jp - 3]))) |
+              as_u32(__builtin_elementwise_sub_sat(mx, as_u16x2(s_skip[3 * jp - 2]))) |
+              as_u32(__builtin_elementwise_sub_sat(as_u16x2(s_skip[3 * jp - 1]), mn));
+          skip0 = __ballot((t & 0xffffu) != 0u) == 0;
+          skip1 = __ballot((t >> 16) != 0u) == 0;
+        }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           __builtin_amdgcn_sched_barrier(0);  // one column at a time
           const int col = 2 * jp + h;
+          if (h ? skip1 : skip0) {  // wave-uniform: 8 zero screen bits
+            if (col < 4)
+              ca <<= 8;
+            else
+              cb <<= 8;
+            continue;
+          }
           float x[8];
 #pragma unroll
           for (int r = 0; r < 8; r++)

@@ -32,7 +32,12 @@ def _src():
 
 
 def _int_array(name):
-    body = re.search(name + r"\[\d+\]\s*=\s*\{([^}]*)\}", _src()).group(1)
+    src = _src().replace("\\\n", "\n")  # join macro continuation lines
+    m = re.search(name + r"\[\d+\]\s*=\s*\{([^}]*)\}", src)
+    if m is None:  # initialised from a macro: `kName[N] = MACRO;` and `#define MACRO {...}`
+        macro = re.search(name + r"\[\d+\]\s*=\s*(\w+)\s*;", src).group(1)
+        m = re.search(r"#define\s+" + macro + r"\s*\{([^}]*)\}", src)
+    body = m.group(1)
     return [int(eval(x)) for x in body.replace("\n", " ").split(",") if x.strip()]
 
 
@@ -185,3 +190,49 @@ def test_screen_thresholds_are_conservative():
                     # the kernel's fp32 sum differs from s_exact by < 2^9 (see kernels.hip)
                     slack = 0 if r in (0, 4) else 512  # rows 0/4 are exact in fp32
                     assert abs(s_exact[r]) - slack > B, (q, n, s_exact[r], B)
+
+
+def _skip_limits(q, col):
+    """Python restatement of open_ctx's k_encode column-skip limits (Rmax, A) for a column."""
+    dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
+    qm = oracle.matrix(q)[1].astype(np.int64)
+    rmax, amax = 65535, 0
+    for ro in range(8):
+        T = ((5 << 18) + qm[ro * 8 + col] - 1) // qm[ro * 8 + col]
+        if ro == 0:
+            amax = max(0, 2 * T - 2)
+        elif ro == 4:
+            rmax = min(rmax, 4 * T - 3)
+        else:
+            rmax = min(rmax, (2 * (T * 131072 - 65536 - 1)) // int(np.abs(dot[ro]).sum()))
+    return max(0, rmax), amax
+
+
+@pytest.mark.parametrize("q", [1, 2, 3, 5, 8, 13, 31])
+def test_column_skip_limits_are_sound(q):
+    """A column whose row-pass values satisfy k_encode's skip test (max - min <= Rmax,
+    |u| <= A) has every pass-2 output quantising to zero: checked on the extreme columns
+    (values at the box corners with the sign pattern of each output row) and random ones."""
+    dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
+    add = np.array([8, 1 << 16, 1 << 16, 1 << 16, 8, 1 << 16, 1 << 16, 1 << 16], np.int64)
+    sh = np.array([4, 17, 17, 17, 4, 17, 17, 17])
+    qm = oracle.matrix(q)[1].astype(np.int64)
+    rng = np.random.default_rng(q)
+    for col in range(2, 8):
+        rmax, a = _skip_limits(q, col)
+        r = min(rmax, 2 * a)
+        T = ((5 << 18) + qm[np.arange(8) * 8 + col] - 1) // qm[np.arange(8) * 8 + col]
+        cols = []
+        for k in range(8):
+            s = dot[k] > 0
+            for lo in (-a, a - r, (a - r - a) // 2):
+                cols += [lo + r * s, lo + r * ~s]
+        cols += list(rng.integers(-a, a + 1, (200, 8)))
+        for u in cols:
+            u = np.asarray(u, np.int64)
+            assert u.max() - u.min() <= rmax and np.abs(u).max() <= a
+            v = (dot @ u + add) >> sh
+            assert (np.abs(v) < T).all(), (q, col, u, v, T)
+        # and the limits are not vacuous at typical quality
+        if q <= 8:
+            assert rmax > 0 and a > 0
