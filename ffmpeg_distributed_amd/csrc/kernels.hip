@@ -233,38 +233,23 @@ __device__ __forceinline__ int dc_cat(int diff) {
   return diff == 0 ? 0 : 32 - __clz(a);
 }
 
-// First emission pass: the block's bits left-aligned in up to 4 register words (a
-// block's offset in the chunk is not known yet); counts every bit even past 4 words.
-struct RegSink {
+// First emission pass: the block's last 128 bits right-aligned in a 4-register shift
+// register (w3 lowest; the block's offset in the chunk is not known yet), and the total bit
+// count (blocks over 128 bits are re-emitted by SlotSink).  Branch-free: appending n <= 26
+// bits is four funnel shifts, (w_i << n) | (w_i+1 >> (32 - n)), one v_alignbit each.
+struct ShiftSink {
   MJG_SINK_SYMBOLS
-  uint64_t acc = 0;
-  int nacc = 0;
-  uint32_t bits = 0, nw = 0;
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  uint32_t bits = 0;
   __device__ __forceinline__ void emit(uint32_t v, int n) {
-    acc = (acc << n) | v;
-    nacc += n;
+    const uint32_t sh = 32u - (uint32_t)n;
+    w0 = __builtin_amdgcn_alignbit(w0, w1, sh);
+    w1 = __builtin_amdgcn_alignbit(w1, w2, sh);
+    w2 = __builtin_amdgcn_alignbit(w2, w3, sh);
+    w3 = __builtin_amdgcn_alignbit(w3, v << sh, sh);
     bits += (uint32_t)n;
-    if (nacc >= 32) {
-      nacc -= 32;
-      const uint32_t w = (uint32_t)(acc >> nacc);
-      w0 = nw == 0 ? w : w0;
-      w1 = nw == 1 ? w : w1;
-      w2 = nw == 2 ? w : w2;
-      w3 = nw == 3 ? w : w3;
-      nw++;
-    }
   }
-  __device__ __forceinline__ void finish() {
-    if (nacc > 0) {
-      const uint32_t w = (uint32_t)(acc << (32 - nacc));
-      w0 = nw == 0 ? w : w0;
-      w1 = nw == 1 ? w : w1;
-      w2 = nw == 2 ? w : w2;
-      w3 = nw == 3 ? w : w3;
-      nw++;
-    }
-  }
+  __device__ __forceinline__ void finish() {}
 };
 
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
@@ -807,7 +792,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     }
     const uint32_t *act = MODE == kEmitFrame ? s_aux + tab * 256 : s_ac + tab * 256;
     const uint32_t *dct = MODE == kEmitFrame ? s_aux + 512 + tab * 16 : s_dc + tab * 16;
-    RegSink q;
+    ShiftSink q;
     q.act = act;
     q.dct = dct;
 #if MJG_ABLATE == 0 || MJG_ABLATE == 4
@@ -837,19 +822,19 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     uint32_t head = 0, tail = 0;
     if (has && MJG_ABLATE != 4) {
       if (q.bits <= 128) {
-        const uint32_t w[5] = {q.w0, q.w1, q.w2, q.w3, 0u};
-        head = w[0] >> sft;
+        // the block's words from its end: d[4] = word lw, d[4 - j] = word lw - j, i.e. the
+        // right-aligned 128 bits shifted left by t, the free bits after the block in word lw
+        const uint32_t t = (32u - ((off + q.bits) & 31u)) & 31u, sh = 32u - t;  // sh in 1..32
+        const uint32_t d[5] = {(uint32_t)((uint64_t)q.w0 >> sh),
+                               (uint32_t)((((uint64_t)q.w0 << 32) | q.w1) >> sh),
+                               (uint32_t)((((uint64_t)q.w1 << 32) | q.w2) >> sh),
+                               (uint32_t)((((uint64_t)q.w2 << 32) | q.w3) >> sh), q.w3 << t};
         const uint32_t nmid = lw - fw;  // 0..4
+        tail = d[4];
 #pragma unroll
-        for (int i = 1; i < 5; i++) {
-          if ((uint32_t)i <= nmid) {
-            const uint32_t v = sft ? (w[i] >> sft) | (w[i - 1] << (32 - sft)) : w[i];
-            if ((uint32_t)i < nmid)
-              slot[fw + i] = v;
-            else
-              tail = v;
-          }
-        }
+        for (int j = 1; j < 4; j++)
+          if ((uint32_t)j < nmid) slot[lw - j] = d[4 - j];
+        head = nmid == 0 ? d[4] : nmid == 1 ? d[3] : nmid == 2 ? d[2] : nmid == 3 ? d[1] : d[0];
       } else {  // long block: re-emit, interior words straight to the slot
         SlotSink sink;
         sink.act = act;
