@@ -31,7 +31,8 @@
 #define MJG_RC_LUT 1  // tv->pc range conversion through a 512-byte LDS table (0: fp32 fma + med3)
 #endif
 #ifndef MJG_ABLATE
-#define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store
+#define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store,
+                      // 5 candidates not quantised exactly (v = 1 or 2)
 #endif
 
 namespace mjg {
@@ -49,7 +50,8 @@ constexpr float kRnd = 0x1p-10f;
 
 // jfdctint pass 2 (CONST_BITS 13, PASS1_BITS 4) per output row as one dot product over
 // the 8 column inputs: the LLM butterfly's t/z terms multiplied out (rows 0/4: +-1 with
-// DESCALE 4; others: DESCALE 17).  kPass2Add: rounding constant minus 32768 * row sum
+// DESCALE 4; others: DESCALE 17).  kPass2Add (tests only: the kernel xors the bias away):
+// rounding constant minus 32768 * row sum
 // (the u16 row image carries +32768).
 #define MJG_PASS2_DOT                                                  \
   {1, 1, 1, 1, 1, 1, 1, 1,                                             \
@@ -255,22 +257,29 @@ struct ShiftSink {
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
 // image (pkcol = s_pk + lane: word [r*4 + c/2] holds rows r, columns c, c+1 as u16 = value
 // + 32768).  jfdctint pass 2 for output row ro is one integer dot product over the column
-// (the LLM butterfly's products and sums folded into m2[ro][*]; every partial sum wraps
-// mod 2^32 and the true sum fits int32), then DESCALE and dct_quantize_c's intra rounding:
-// sign(u) * ((|u| * qmat + 3<<18) >> 21), folded into one signed multiply-add.
-__device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const int *m2,
+// (the LLM butterfly's products and sums folded into kPass2Dot[ro][*]): v_perm gathers the
+// column's rows r, r+1 into one word, the xor with 0x8000 per half turns value + 32768 into
+// the signed value, and v_dot2_i32_i16 multiplies two rows at a time against the packed
+// coefficient pairs m2p[ro][*] (exact: every product and sum fits int32).  Then DESCALE and
+// dct_quantize_c's intra rounding: sign(u) * ((|u| * qmat + 3<<18) >> 21), folded into one
+// signed multiply-add.
+typedef short short2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const uint32_t *m2p,
                                           const int *qc) {
   const int ro = n >> 3, c = n & 7;
-  const uint32_t sh16 = (uint32_t)(c & 1) << 4;
-  const int4 ma = *(const int4 *)(m2 + ro * 8), mb = *(const int4 *)(m2 + ro * 8 + 4);
-  const int m[8] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
-  int acc = m2[64 + ro];  // rounding constant and the -32768 bias of the u16 image
+  const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
+  const uint4 mp = *(const uint4 *)(m2p + ro * 4);
+  const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
+  const bool dc_row = ro == 0 || ro == 4;
+  int acc = dc_row ? 8 : (1 << 16);
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
-    const int hv = (int)((pkcol[(r * 4 + (c >> 1)) * 64] >> sh16) & 0xffffu);
-    acc = __mul24(hv, m[r]) + acc;
+  for (int i = 0; i < 4; i++) {
+    const uint32_t w0 = pkcol[((2 * i) * 4 + (c >> 1)) * 64], w1 = pkcol[((2 * i + 1) * 4 + (c >> 1)) * 64];
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel) ^ 0x80008000u;
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
+                                 false);
   }
-  const int u = acc >> (ro == 0 || ro == 4 ? 4 : 17);
+  const int u = acc >> (dc_row ? 4 : 17);
   const int qm = qc[c * 8 + ro];
   return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
 }
@@ -283,7 +292,7 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const in
 // testsrc2 4K q5, so the loop is short.)
 template <class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
-                                           const uint8_t *zz, const int *m2, const int *qc,
+                                           const uint8_t *zz, const uint32_t *m2, const int *qc,
                                            Sink &sink) {
   {
     const int cat = dc_cat(diff);
@@ -293,7 +302,11 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
   while (cand) {
     const int k = (int)__builtin_ctzll(cand);
     cand &= cand - 1;
+#if MJG_ABLATE == 5
+    const int v = 1 + (k & 1);
+#else
     const int v = exact_coef(pkcol, zz[k], m2, qc);
+#endif
     if (v == 0) continue;  // screened in, quantises to zero
     int run = k - prev - 1;
     prev = k;
@@ -464,7 +477,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
-  __shared__ __attribute__((aligned(16))) int s_m2[72];       // pass-2 dot rows + per-row constant
+  __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
   __shared__ uint8_t s_rc[MJG_RC_LUT ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
@@ -480,11 +493,11 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
     s_thr[tid] = __uint_as_float(tabs[608 + tid]);
-    s_m2[tid] = kPass2Dot[tid];
+    if (tid < 32)
+      s_m2[tid] = (uint32_t)(uint16_t)kPass2Dot[2 * tid] | ((uint32_t)(uint16_t)kPass2Dot[2 * tid + 1] << 16);
     s_scat[tid] = kScreenScatter[tid];
   }
   if (tid < 8) {
-    s_m2[64 + tid] = kPass2Add[tid];
     s_desc[tid] = tabs[672 + tid];
   }
   if (tid < 12) s_skip[tid] = tabs[680 + tid];
