@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--seg", type=int, default=None)
     p.add_argument("--cpu-sample-frames", type=int, default=96)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
+    p.add_argument("--kernel-timing-detail", action="store_true",
+                   help="events around every tail kernel too (adds ~10 us idle per event)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_encode_4k_q5.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py")
     return p.parse_args()
@@ -155,22 +158,36 @@ def main():
 
     if a.rst:
         HUFF = "default"  # slice threading forces the default tables
-    enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg, timing=True,
+    enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg,
+                       timing=False if a.no_kernel_timing else ("detail" if a.kernel_timing_detail else True),
                        huffman=HUFF, rst=a.rst)
     bytes_out = []
 
+    # Segments are pipelined two deep (mjg_submit queues up to two): segment s+1's kernels
+    # are queued behind segment s's before s is synced, so the GPU does not idle while the
+    # host collects a segment's sizes and issues the next launches.
     def step(s):
         base = pool[(s % nseg_pool) * seg]
         enc.submit(device_ptr=base.data_ptr(), nframes=seg)
-        sizes = enc.sync()
-        bytes_out.append(int(sizes.sum()))
+        if enc.pending == 2:
+            bytes_out.append(int(enc.sync().sum()))
+
+    def drain_and_sync():
+        while enc.pending:
+            bytes_out.append(int(enc.sync().sum()))
+        torch.cuda.synchronize()
 
     def reset():
+        drain_and_sync()
         enc.kernel_times(reset=True)
         bytes_out.clear()
 
-    dt = timed_region(step, a.warmup, a.steps, barrier, torch.cuda.synchronize, reset)
-    kt, nl = enc.kernel_times()
+    dt = timed_region(step, a.warmup, a.steps, barrier, drain_and_sync, reset)
+    if a.no_kernel_timing:
+        from ffmpeg_distributed_amd._lib import KERNEL_NAMES
+        kt, nl = {k: 0.0 for k in KERNEL_NAMES}, 0
+    else:
+        kt, nl = enc.kernel_times()
     dt = max_over_ranks(dt, dist if world > 1 else None, dev)
 
     frames_total = a.steps * seg * world

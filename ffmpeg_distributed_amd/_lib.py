@@ -26,11 +26,12 @@ MJG_F_SWS_NO_BITEXACT = 4
 MJG_F_COM_ITU601 = 8
 MJG_F_HUFFMAN_OPTIMAL = 16
 MJG_F_RST = 32
+MJG_F_TIMING_DETAIL = 64
 
 # mjg_config.chroma_format
 CHROMA_FORMATS = {"420": 0, "422": 1, "444": 2}
 
-KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write", "huff")
+KERNEL_NAMES = ("scale", "encode", "scan_bits", "count_ff", "scan_ff", "write", "huff", "tail")
 MJG_NUM_KERNELS = len(KERNEL_NAMES)
 
 # Every symbol include/mjgpu.h declares (checked by tests/test_abi.py).

@@ -152,6 +152,31 @@ struct PlaneScale {
   dim3 grid;
 };
 
+// Per-submit state.  A context has two slots so a second mjg_submit can be queued before
+// the first is synced (the kernels of both run back to back on the ctx stream); everything
+// a submit's results and its overflow re-write need lives in its slot.  Slot 1 is
+// allocated on the first pipelined submit.
+struct Slot {
+  bool alloc = false, pending = false;
+  int n = 0;
+  uint64_t total = 0;
+  uint32_t *d_scratch = nullptr;
+  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
+  uint32_t *d_frame_bits = nullptr, *d_status = nullptr;
+  uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
+  uint64_t *d_seg_size = nullptr;  // RST mode: stuffed segment sizes and offsets after the header
+  uint32_t *d_seg_off = nullptr;
+  uint8_t *d_out = nullptr;
+  size_t out_cap = 0;
+  uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;  // optimal
+  uint8_t *d_dht = nullptr;
+  int16_t *d_dbg = nullptr;
+  uint64_t *h_sizes = nullptr;
+  uint32_t *h_status = nullptr;
+  hipEvent_t done = nullptr;
+  hipEvent_t ev[MJG_NUM_KERNELS][2] = {};
+};
+
 }  // namespace
 
 struct mjg_ctx {
@@ -169,32 +194,20 @@ struct mjg_ctx {
   uint32_t *d_tabs = nullptr;
   uint8_t *d_hdr = nullptr;
   uint8_t *d_stage = nullptr, *d_scaled = nullptr;
-  uint32_t *d_scratch = nullptr;
-  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
-  uint32_t *d_frame_bits = nullptr, *d_status = nullptr, *d_work = nullptr;
-  uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
-  // RST mode: per-segment stuffed sizes and their offsets after the frame header
-  bool rst = false;
-  uint64_t *d_seg_size = nullptr;
-  uint32_t *d_seg_off = nullptr;
-  uint8_t *d_out = nullptr;
-  size_t out_cap = 0;
-  // -huffman optimal
-  bool optimal = false;
+  uint32_t *d_work = nullptr;  // k_encode's batch counter (reset by the scan kernels)
+  bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
+  bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
-  uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;
-  uint8_t *d_dht = nullptr;
-  int16_t *d_dbg = nullptr;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
+  size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
 
-  uint64_t *h_sizes = nullptr;
-  uint32_t *h_status = nullptr;
-  int last_n = 0;
-  bool pending = false, synced = false;
-  uint64_t last_total = 0;
+  Slot slot[2];
+  int head = 0;   // slot of the next submit
+  int nout = 0;   // submits queued and not synced (0..2)
+  int last = -1;  // slot of the last synced submit (fetch / output_device / debug read it)
+  bool synced_since_submit = false;
 
-  bool timing = false;
-  hipEvent_t ev[MJG_NUM_KERNELS][2];
+  bool timing = false, timing_detail = false;
   double t_acc[MJG_NUM_KERNELS] = {0};
   int t_n = 0;
 };
@@ -205,21 +218,25 @@ void free_ctx(mjg_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_scratch, c->d_chunk_bits,
-                  c->d_chunk_off, c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_status, c->d_work,
-                  c->d_frame_size, c->d_frame_offsets, c->d_out, c->d_dbg, c->d_hist, c->d_ftabs,
-                  c->d_dht_nval, c->d_hdr_lens, c->d_dht, c->d_seg_size, c->d_seg_off, c->ps[0].hcp,
+  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_work, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
                   c->ps[1].vps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
-  if (c->h_sizes) (void)hipHostFree(c->h_sizes);
-  if (c->h_status) (void)hipHostFree(c->h_status);
-  if (c->timing)
-    for (auto &e : c->ev) {
-      (void)hipEventDestroy(e[0]);
-      (void)hipEventDestroy(e[1]);
+  for (Slot &S : c->slot) {
+    void *sp[] = {S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+                  S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_out,
+                  S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg};
+    for (void *p : sp)
+      if (p) (void)hipFree(p);
+    if (S.h_sizes) (void)hipHostFree(S.h_sizes);
+    if (S.h_status) (void)hipHostFree(S.h_status);
+    if (S.done) (void)hipEventDestroy(S.done);
+    for (auto &e : S.ev) {
+      if (e[0]) (void)hipEventDestroy(e[0]);
+      if (e[1]) (void)hipEventDestroy(e[1]);
     }
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -287,6 +304,40 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   HIP_TRY(hipMemcpy(p.vcp, vcp.data(), vcp.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(p.vps, vps.data(), (size_t)dh * 4, hipMemcpyHostToDevice));
   (void)c;
+  return MJG_OK;
+}
+
+int alloc_slot(mjg_ctx *c, Slot &S) {
+  const size_t B = c->slot_B, NC = c->slot_NC, NS = c->slot_NS;
+  const EncGeom &g = c->geom;
+  int rc;
+  if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||
+      (rc = dmalloc(&S.d_chunk_bits, B * NC)) || (rc = dmalloc(&S.d_chunk_off, B * NC)) ||
+      (rc = dmalloc(&S.d_group_ff, B * NC)) || (rc = dmalloc(&S.d_ff_off, B * NC)) ||
+      (rc = dmalloc(&S.d_frame_bits, B * NS)) || (rc = dmalloc(&S.d_status, 4)) ||
+      (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)))
+    return rc;
+  if (c->rst && ((rc = dmalloc(&S.d_seg_size, B * NS)) || (rc = dmalloc(&S.d_seg_off, B * NS)))) return rc;
+  S.out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096 + 2 * NS);
+  if ((rc = dmalloc(&S.d_out, S.out_cap))) return rc;
+  if (c->optimal &&
+      ((rc = dmalloc(&S.d_hist, B * kFrameTabWords)) || (rc = dmalloc(&S.d_ftabs, B * kFrameTabWords)) ||
+       (rc = dmalloc(&S.d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&S.d_dht_nval, B * 4)) ||
+       (rc = dmalloc(&S.d_hdr_lens, B))))
+    return rc;
+  if (g.debug_coefs && (rc = dmalloc(&S.d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
+#ifdef MJG_STAMPS
+  if (!S.d_dbg && (rc = dmalloc(&S.d_dbg, (size_t)1 << 22))) return rc;  // 512K stamps
+#endif
+  HIP_TRY(hipHostMalloc((void **)&S.h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void **)&S.h_status, 16, hipHostMallocDefault));
+  HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+  if (c->timing)
+    for (auto &e : S.ev) {
+      HIP_TRY(hipEventCreate(&e[0]));
+      HIP_TRY(hipEventCreate(&e[1]));
+    }
+  S.alloc = true;
   return MJG_OK;
 }
 
@@ -438,31 +489,18 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
   int rc;
   if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
-      (rc = dmalloc(&c->d_scratch, B * NC * (size_t)kSlotWords)) ||
-      (rc = dmalloc(&c->d_chunk_bits, B * NC)) || (rc = dmalloc(&c->d_chunk_off, B * NC)) ||
-      (rc = dmalloc(&c->d_group_ff, B * NC)) || (rc = dmalloc(&c->d_ff_off, B * NC)) ||
-      (rc = dmalloc(&c->d_frame_bits, B * NS)) || (rc = dmalloc(&c->d_status, 4)) ||
-      (rc = dmalloc(&c->d_work, 1)) ||
-      (rc = dmalloc(&c->d_frame_size, B)) || (rc = dmalloc(&c->d_frame_offsets, B + 1)))
+      (rc = dmalloc(&c->d_work, 1)))
     return rc;
-  if (c->rst && ((rc = dmalloc(&c->d_seg_size, B * NS)) || (rc = dmalloc(&c->d_seg_off, B * NS)))) return rc;
-  c->out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096 + 2 * NS);
-  if ((rc = dmalloc(&c->d_out, c->out_cap))) return rc;
+  c->slot_B = B;
+  c->slot_NC = NC;
+  c->slot_NS = NS;
+  c->timing = (k.flags & (MJG_F_TIMING | MJG_F_TIMING_DETAIL)) != 0;
+  c->timing_detail = (k.flags & MJG_F_TIMING_DETAIL) != 0;
+  if ((rc = alloc_slot(c, c->slot[0]))) return rc;
   if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
-  if (c->optimal &&
-      ((rc = dmalloc(&c->d_hist, B * kFrameTabWords)) || (rc = dmalloc(&c->d_ftabs, B * kFrameTabWords)) ||
-       (rc = dmalloc(&c->d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&c->d_dht_nval, B * 4)) ||
-       (rc = dmalloc(&c->d_hdr_lens, B))))
-    return rc;
-  if (g.debug_coefs && (rc = dmalloc(&c->d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
-#ifdef MJG_STAMPS
-  if (!c->d_dbg && (rc = dmalloc(&c->d_dbg, (size_t)1 << 22))) return rc;  // 512K stamps
-#endif
   HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(c->d_work, 0, sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipHostMalloc((void **)&c->h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void **)&c->h_status, 16, hipHostMallocDefault));
 
   if (c->scale) {
     const bool bitexact = !(k.flags & MJG_F_SWS_NO_BITEXACT);
@@ -489,52 +527,55 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
 
-  c->timing = (k.flags & MJG_F_TIMING) != 0;
-  if (c->timing)
-    for (auto &e : c->ev) {
-      HIP_TRY(hipEventCreate(&e[0]));
-      HIP_TRY(hipEventCreate(&e[1]));
-    }
   return MJG_OK;
 }
 
-void tmark(mjg_ctx *c, int k, int end) {
-  if (c->timing) (void)hipEventRecord(c->ev[k][end], c->stream);
+// HIP events: with MJG_F_TIMING around scale, huff, encode and the whole tail (scan .. write,
+// reported as MJG_K_TAIL); with MJG_F_TIMING_DETAIL around every kernel (each event record
+// costs ~10 us of GPU idle between the short tail kernels).
+void tmark(mjg_ctx *c, Slot &S, int k, int end) {
+  if (!c->timing) return;
+  const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
+  if (tail && !c->timing_detail) return;
+  (void)hipEventRecord(S.ev[k][end], c->stream);
 }
 
-int launch_write(mjg_ctx *c, int n) {
+// status: reset the overflow flag first (the regrow path; a submit's scan kernel resets it)
+int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
   const EncGeom &g = c->geom;
   const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n * g.nseg;
-  HIP_TRY(hipMemsetAsync(c->d_status, 0, 4, c->stream));
-  tmark(c, MJG_K_WRITE, 0);
-  k_frame_hdr<<<n, 64, 0, c->stream>>>(c->d_frame_size, c->d_hdr, (int)c->hdr.size(), c->d_out,
-                                       (uint64_t)c->out_cap, c->d_frame_offsets, c->d_status,
-                                       c->optimal ? c->d_hdr_lens : nullptr, (int)c->dht_pos,
-                                       (int)c->dht_end, c->d_dht, c->d_dht_nval, c->d_seg_off,
-                                       c->d_seg_size, g.nseg);
+  if (reset_status) HIP_TRY(hipMemsetAsync(S.d_status, 0, 4, c->stream));
+  tmark(c, S, MJG_K_WRITE, 0);
+  k_frame_hdr<<<n, 64, 0, c->stream>>>(S.d_frame_size, c->d_hdr, (int)c->hdr.size(), S.d_out,
+                                       (uint64_t)S.out_cap, S.d_frame_offsets, S.d_status,
+                                       c->optimal ? S.d_hdr_lens : nullptr, (int)c->dht_pos,
+                                       (int)c->dht_end, S.d_dht, S.d_dht_nval, S.d_seg_off,
+                                       S.d_seg_size, g.nseg);
   k_write<<<(ngroups + 3) / 4, 256, 0, c->stream>>>(
-      c->d_scratch, c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, c->d_ff_off, c->d_frame_size,
-      c->d_frame_offsets, (int)c->hdr.size(), c->optimal ? c->d_hdr_lens : nullptr, g.nchunks, gpf,
-      ngroups, c->d_out, (uint64_t)c->out_cap, c->d_seg_off, g.nseg);
-  tmark(c, MJG_K_WRITE, 1);
+      S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, S.d_ff_off, S.d_frame_size,
+      S.d_frame_offsets, (int)c->hdr.size(), c->optimal ? S.d_hdr_lens : nullptr, g.nchunks, gpf,
+      ngroups, S.d_out, (uint64_t)S.out_cap, S.d_seg_off, g.nseg);
+  tmark(c, S, MJG_K_WRITE, 1);
+  if (c->timing && !c->timing_detail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->stream);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(c->h_sizes, c->d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
+  HIP_TRY(hipMemcpyAsync(S.h_sizes, S.d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
                          c->stream));
-  HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(S.h_status, S.d_status, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(S.done, c->stream));
   return MJG_OK;
 }
 
 template <int MODE>
-void launch_encode(mjg_ctx *c, const uint8_t *enc_in, int wgs, int ntasks) {
+void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
   if (g.range_convert)
     k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
-        enc_in, g, c->d_tabs, c->d_scratch, c->d_chunk_bits, c->d_dbg, c->d_work, ntasks, c->d_hist,
-        c->d_ftabs);
+        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, c->d_work, ntasks, S.d_hist,
+        S.d_ftabs);
   else
     k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
-        enc_in, g, c->d_tabs, c->d_scratch, c->d_chunk_bits, c->d_dbg, c->d_work, ntasks, c->d_hist,
-        c->d_ftabs);
+        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, c->d_work, ntasks, S.d_hist,
+        S.d_ftabs);
 }
 
 }  // namespace
@@ -583,9 +624,14 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (!c || !frames) return set_err(MJG_E_INVALID, "null argument");
   if (n < 1 || n > c->cfg.max_batch)
     return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
-  if (c->pending) return set_err(MJG_E_STATE, "previous submit not synced");
+  if (c->nout == 2) return set_err(MJG_E_STATE, "two submits queued: sync one first");
   HIP_TRY(hipSetDevice(c->device));
   const EncGeom &g = c->geom;
+  Slot &S = c->slot[c->head];
+  if (!S.alloc) {  // the second slot, on the first pipelined submit
+    const int rc = alloc_slot(c, S);
+    if (rc) return rc;
+  }
   const uint8_t *src = frames;
   if (!src_is_device) {
     if (!c->d_stage) {  // staging for host submits, allocated on first use
@@ -598,7 +644,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   }
   const uint8_t *enc_in = src;
   if (c->scale) {
-    tmark(c, MJG_K_SCALE, 0);
+    tmark(c, S, MJG_K_SCALE, 0);
     const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
     for (int p = 0; p < 3; p++) {
       PlaneScale &ps = c->ps[p ? 1 : 0];
@@ -619,7 +665,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       else
         k_scale<0, 0><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
     }
-    tmark(c, MJG_K_SCALE, 1);
+    tmark(c, S, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());
     enc_in = c->d_scaled;
   }
@@ -627,111 +673,128 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   const int nsegs = g.nseg * n;  // entropy-coded segments of this submit
   const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
   if (c->optimal) {  // pass 1: symbol counts per frame, then the frame's tables
-    tmark(c, MJG_K_HUFF, 0);
-    HIP_TRY(hipMemsetAsync(c->d_hist, 0, (size_t)n * kFrameTabWords * 4, c->stream));
-    launch_encode<kCount>(c, enc_in, wgs, ntasks);
+    tmark(c, S, MJG_K_HUFF, 0);
+    HIP_TRY(hipMemsetAsync(S.d_hist, 0, (size_t)n * kFrameTabWords * 4, c->stream));
+    launch_encode<kCount>(c, S, enc_in, wgs, ntasks);
     HIP_TRY(hipMemsetAsync(c->d_work, 0, 4, c->stream));  // batch counter for pass 2
-    k_huff_build<<<n * 4, 64, 0, c->stream>>>(c->d_hist, c->d_ftabs, c->d_dht, c->d_dht_nval);
-    tmark(c, MJG_K_HUFF, 1);
+    k_huff_build<<<n * 4, 64, 0, c->stream>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
+    tmark(c, S, MJG_K_HUFF, 1);
     HIP_TRY(hipGetLastError());
   }
-  tmark(c, MJG_K_ENCODE, 0);
+  tmark(c, S, MJG_K_ENCODE, 0);
   if (c->optimal)
-    launch_encode<kEmitFrame>(c, enc_in, wgs, ntasks);
+    launch_encode<kEmitFrame>(c, S, enc_in, wgs, ntasks);
   else
-    launch_encode<kEmitDefault>(c, enc_in, wgs, ntasks);
-  tmark(c, MJG_K_ENCODE, 1);
+    launch_encode<kEmitDefault>(c, S, enc_in, wgs, ntasks);
+  tmark(c, S, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
-  tmark(c, MJG_K_SCAN_BITS, 0);
+  if (c->timing && !c->timing_detail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->stream);
+  tmark(c, S, MJG_K_SCAN_BITS, 0);
   if (c->rst)
-    k_scan_bits_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits,
-                                                            g.nchunks, nsegs, c->d_work);
+    k_scan_bits_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits,
+                                                            g.nchunks, nsegs, c->d_work, S.d_status);
   else
-    k_scan_bits<<<n, 1024, 0, c->stream>>>(c->d_chunk_bits, c->d_chunk_off, c->d_frame_bits, g.nchunks,
-                                           c->d_work);
-  tmark(c, MJG_K_SCAN_BITS, 1);
+    k_scan_bits<<<n, 1024, 0, c->stream>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, g.nchunks,
+                                           c->d_work, S.d_status);
+  tmark(c, S, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
-  tmark(c, MJG_K_COUNT_FF, 0);
+  tmark(c, S, MJG_K_COUNT_FF, 0);
   const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
-  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->stream>>>(c->d_scratch, c->d_chunk_bits, c->d_chunk_off,
-                                                           c->d_frame_bits, c->d_group_ff, g.nchunks,
+  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->stream>>>(S.d_scratch, S.d_chunk_bits, S.d_chunk_off,
+                                                           S.d_frame_bits, S.d_group_ff, g.nchunks,
                                                            gpf, gpf * nsegs);
-  tmark(c, MJG_K_COUNT_FF, 1);
+  tmark(c, S, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
-  tmark(c, MJG_K_SCAN_FF, 0);
+  tmark(c, S, MJG_K_SCAN_FF, 0);
   // optimal: header = default header - its 348 table values + the frame's
   if (c->rst) {  // segment sizes (each with its RSTn / EOI trailer), then per-frame offsets
-    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits,
-                                                          c->d_seg_size, gpf, nsegs);
-    k_seg_sizes<<<n, 64, 0, c->stream>>>(c->d_seg_size, g.nseg, (int)c->hdr.size(), c->d_seg_off,
-                                         c->d_frame_size);
+    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+                                                          S.d_seg_size, gpf, nsegs);
+    k_seg_sizes<<<n, 64, 0, c->stream>>>(S.d_seg_size, g.nseg, (int)c->hdr.size(), S.d_seg_off,
+                                         S.d_frame_size);
   } else {
-    k_scan_ff<<<n, 1024, 0, c->stream>>>(c->d_group_ff, c->d_ff_off, c->d_frame_bits, c->d_frame_size,
-                                         gpf, (int)c->hdr.size(), c->optimal ? c->d_dht_nval : nullptr,
-                                         (int)c->hdr.size() - 348, c->d_hdr_lens);
+    k_scan_ff<<<n, 1024, 0, c->stream>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, S.d_frame_size,
+                                         gpf, (int)c->hdr.size(), c->optimal ? S.d_dht_nval : nullptr,
+                                         (int)c->hdr.size() - 348, S.d_hdr_lens);
   }
-  tmark(c, MJG_K_SCAN_FF, 1);
+  tmark(c, S, MJG_K_SCAN_FF, 1);
   HIP_TRY(hipGetLastError());
-  int rc = launch_write(c, n);
+  int rc = launch_write(c, S, n, false);
   if (rc) return rc;
-  c->last_n = n;
-  c->pending = true;
-  c->synced = false;
+  S.n = n;
+  S.pending = true;
+  c->head ^= 1;
+  c->nout++;
+  c->synced_since_submit = false;
   return MJG_OK;
 }
 
+// Completes the oldest queued submit (or, with none queued, reports the last synced one).
 int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
   if (!c) return set_err(MJG_E_INVALID, "null ctx");
-  if (!c->pending && !c->synced) return set_err(MJG_E_STATE, "nothing submitted");
+  if (c->nout == 0 && c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
   HIP_TRY(hipSetDevice(c->device));
-  if (c->pending) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    const int n = c->last_n;
+  if (c->nout > 0) {
+    const int si = c->nout == 2 ? c->head : c->head ^ 1;  // oldest queued submit
+    Slot &S = c->slot[si];
+    HIP_TRY(hipEventSynchronize(S.done));
+    const int n = S.n;
     uint64_t t = 0;
-    for (int i = 0; i < n; i++) t += c->h_sizes[i];
-    if (*c->h_status & 1u) {  // packed output overflowed: grow, re-run the write pass only
-      HIP_TRY(hipFree(c->d_out));
-      c->d_out = nullptr;
-      c->out_cap = t + t / 4 + 4096;
-      int rc = dmalloc(&c->d_out, c->out_cap);
+    for (int i = 0; i < n; i++) t += S.h_sizes[i];
+    if (*S.h_status & 1u) {  // packed output overflowed: grow, re-run the write pass only
+      HIP_TRY(hipFree(S.d_out));
+      S.d_out = nullptr;
+      S.out_cap = t + t / 4 + 4096;
+      int rc = dmalloc(&S.d_out, S.out_cap);
       if (rc) return rc;
-      if ((rc = launch_write(c, n))) return rc;
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (*c->h_status & 1u) return set_err(MJG_E_HIP, "output overflow persisted");
+      if ((rc = launch_write(c, S, n, true))) return rc;
+      HIP_TRY(hipEventSynchronize(S.done));
+      if (*S.h_status & 1u) return set_err(MJG_E_HIP, "output overflow persisted");
     }
     if (c->timing) {
       for (int k = 0; k < MJG_NUM_KERNELS; k++) {
         if (k == MJG_K_SCALE && !c->scale) continue;
         if (k == MJG_K_HUFF && !c->optimal) continue;
+        const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
+        if (tail != c->timing_detail && (tail || k == MJG_K_TAIL)) continue;
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, c->ev[k][0], c->ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
+        if (hipEventElapsedTime(&ms, S.ev[k][0], S.ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
       }
       c->t_n++;
     }
-    c->last_total = t;
-    c->pending = false;
-    c->synced = true;
+    S.total = t;
+    S.pending = false;
+    c->nout--;
+    c->last = si;
   }
-  if (frame_sizes) memcpy(frame_sizes, c->h_sizes, c->last_n * sizeof(uint64_t));
-  if (total) *total = c->last_total;
+  c->synced_since_submit = true;
+  const Slot &L = c->slot[c->last];
+  if (frame_sizes) memcpy(frame_sizes, L.h_sizes, L.n * sizeof(uint64_t));
+  if (total) *total = L.total;
   return MJG_OK;
 }
 
+// Copies the packed JPEGs of the last synced submit; with no mjg_sync since the last
+// mjg_submit it syncs the oldest queued submit first (the submit -> fetch pattern).
 int mjg_fetch(mjg_ctx *c, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  int rc = mjg_sync(c, nullptr, nullptr);
-  if (rc) return rc;
-  if (cap < c->last_total) return set_err(MJG_E_CAPACITY, "fetch needs %llu bytes",
-                                          (unsigned long long)c->last_total);
-  HIP_TRY(hipMemcpyAsync(out, c->d_out, c->last_total, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->nout > 0 && !c->synced_since_submit) {
+    const int rc = mjg_sync(c, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  if (c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
+  const Slot &L = c->slot[c->last];
+  if (cap < L.total) return set_err(MJG_E_CAPACITY, "fetch needs %llu bytes", (unsigned long long)L.total);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(out, L.d_out, L.total, hipMemcpyDeviceToHost));
   return MJG_OK;
 }
 
 int mjg_output_device(mjg_ctx *c, const uint8_t **data, const uint64_t **offsets) {
   if (!c) return set_err(MJG_E_INVALID, "null ctx");
-  if (data) *data = c->d_out;
-  if (offsets) *offsets = c->d_frame_offsets;
+  const Slot &L = c->slot[c->last < 0 ? 0 : c->last];
+  if (data) *data = L.d_out;
+  if (offsets) *offsets = L.d_frame_offsets;
   return MJG_OK;
 }
 
@@ -803,14 +866,18 @@ int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, i
 
 int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  if (!c->d_dbg) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
-  int rc = mjg_sync(c, nullptr, nullptr);
-  if (rc) return rc;
+  if (!c->geom.debug_coefs) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
+  if (c->nout > 0 && !c->synced_since_submit) {
+    const int rc = mjg_sync(c, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  if (c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
+  const Slot &L = c->slot[c->last];
   const size_t nb = (size_t)c->geom.nmcu * c->geom.bpm;  // dbg buffer: frame-major, coding order
-  if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
+  if (frame < 0 || frame >= L.n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
   // the kernel stores each quantised block in natural (raster) order
-  HIP_TRY(hipMemcpy(out, c->d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
+  HIP_TRY(hipMemcpy(out, L.d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
                     hipMemcpyDeviceToHost));
   return MJG_OK;
 }
@@ -818,9 +885,12 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
 int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
   if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale");
-  int rc = mjg_sync(c, nullptr, nullptr);
-  if (rc) return rc;
-  if (frame < 0 || frame >= c->last_n) return set_err(MJG_E_INVALID, "frame %d", frame);
+  if (c->nout > 0) {  // the scaled planes are shared by the slots: only the latest submit's
+    const int rc = mjg_sync(c, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  if (c->nout > 0 || c->last < 0) return set_err(MJG_E_STATE, "sync every queued submit first");
+  if (frame < 0 || frame >= c->slot[c->last].n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (cap < c->enc_frame_bytes) return set_err(MJG_E_CAPACITY, "need %zu bytes", c->enc_frame_bytes);
   HIP_TRY(hipMemcpy(out, c->d_scaled + (size_t)frame * c->enc_frame_bytes, c->enc_frame_bytes,
                     hipMemcpyDeviceToHost));
@@ -845,7 +915,7 @@ int mjg_debug_filter(mjg_ctx *c, int plane, int dir, int16_t *coeff, int32_t *po
 #ifdef MJG_STAMPS
 extern "C" int mjg_debug_stamps(mjg_ctx *c, uint64_t *out, size_t n) {
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipMemcpy(out, c->d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, c->slot[0].d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return MJG_OK;
 }
 #endif

@@ -1154,9 +1154,13 @@ __device__ uint32_t block_excl_scan(const uint32_t *in, uint32_t *out, int n) {
 __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk_bits,
                                                     uint32_t *__restrict__ chunk_off,
                                                     uint32_t *__restrict__ frame_bits, int nchunks,
-                                                    uint32_t *__restrict__ work_ctr) {
+                                                    uint32_t *__restrict__ work_ctr,
+                                                    uint32_t *__restrict__ status) {
   const int f = blockIdx.x;
-  if (f == 0 && threadIdx.x == 0) *work_ctr = 0;  // k_encode's batch counter, for the next launch
+  if (f == 0 && threadIdx.x == 0) {
+    *work_ctr = 0;  // k_encode's batch counter, for the next launch
+    *status = 0;    // output overflow flag, set by k_frame_hdr
+  }
   uint32_t *cb = chunk_bits + (size_t)f * nchunks;
   for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
   __syncthreads();
@@ -1181,9 +1185,13 @@ __device__ __forceinline__ uint32_t wave_excl_scan_arr(const uint32_t *in, uint3
 __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ chunk_bits,
                                                        uint32_t *__restrict__ chunk_off,
                                                        uint32_t *__restrict__ seg_bits, int nchunks,
-                                                       int nsegs, uint32_t *__restrict__ work_ctr) {
+                                                       int nsegs, uint32_t *__restrict__ work_ctr,
+                                                       uint32_t *__restrict__ status) {
   const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *work_ctr = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *work_ctr = 0;
+    *status = 0;
+  }
   if (sg >= nsegs) return;
   uint32_t *cb = chunk_bits + (size_t)sg * nchunks;
   for (int i = lane; i < nchunks; i += 64) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);

@@ -11,6 +11,7 @@ writes.  No CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+from collections import deque
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -62,7 +63,9 @@ class MjpegEncoder:
         self.dst_h = int(dst_h if dst_h is not None else src_h)
         self.max_batch = int(max_batch)
         flags = 0
-        if timing:
+        if timing == "detail":
+            flags |= _lib.MJG_F_TIMING_DETAIL
+        elif timing:
             flags |= _lib.MJG_F_TIMING
         if debug_coefs:
             flags |= _lib.MJG_F_DEBUG_COEFS
@@ -89,7 +92,9 @@ class MjpegEncoder:
         check(self._L.mjg_open(self.device, C.byref(cfg), C.byref(h)))
         self._h = h
         self.frame_bytes = int(self._L.mjg_frame_bytes(h))
-        self._n = 0
+        self._queued = deque()        # (nframes, host buffer kept alive) per queued submit
+        self._synced_since_submit = False
+        self._last_sizes = np.zeros(0, np.uint64)
         self._sizes = np.zeros(self.max_batch + 1, np.uint64)
 
     # ------------------------------------------------------------------ basics
@@ -122,14 +127,21 @@ class MjpegEncoder:
         return bytes(buf)
 
     # ------------------------------------------------------------------ encode
+    @property
+    def pending(self) -> int:
+        """Submits queued and not yet synced (at most 2)."""
+        return len(self._queued)
+
     def submit(self, frames=None, nframes: Optional[int] = None, device_ptr: Optional[int] = None):
-        """Queue `nframes` packed I420 frames: a host buffer (numpy / bytes) or a device
-        pointer (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU)."""
+        """Queue `nframes` packed frames: a host buffer (numpy / bytes) or a device pointer
+        (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU).  Two submits may be queued;
+        their kernels run back to back on the context's stream."""
         if device_ptr is not None:
             if nframes is None:
                 raise ValueError("nframes is required with device_ptr")
             check(self._L.mjg_submit(self._h, C.c_void_p(int(device_ptr)), int(nframes), 1))
-            self._n = int(nframes)
+            self._queued.append((int(nframes), None))
+            self._synced_since_submit = False
             return
         arr = np.ascontiguousarray(np.frombuffer(frames, dtype=np.uint8)
                                    if isinstance(frames, (bytes, bytearray, memoryview))
@@ -138,19 +150,28 @@ class MjpegEncoder:
             raise ValueError(f"buffer of {arr.size} bytes is not a whole number of "
                              f"{self.frame_bytes}-byte frames")
         n = arr.size // self.frame_bytes if nframes is None else int(nframes)
-        self._keep = arr  # the async H2D copy reads it until sync()
         check(self._L.mjg_submit(self._h, C.c_void_p(arr.ctypes.data), n, 0))
-        self._n = n
+        self._queued.append((n, arr))  # the async H2D copy reads arr until its sync
+        self._synced_since_submit = False
 
     def sync(self) -> np.ndarray:
+        """Complete the oldest queued submit; its per-frame JPEG sizes."""
+        if not self._queued:
+            return self._last_sizes.copy()
         total = C.c_uint64()
         check(self._L.mjg_sync(self._h, self._sizes.ctypes.data_as(C.POINTER(C.c_uint64)),
                                C.byref(total)))
-        self._keep = None
-        return self._sizes[: self._n].copy()
+        n, _ = self._queued.popleft()
+        self._synced_since_submit = True
+        self._last_sizes = self._sizes[:n].copy()
+        return self._last_sizes.copy()
 
     def fetch(self) -> List[bytes]:
-        sizes = self.sync()
+        """Packed JPEGs of the last synced submit (syncing the oldest queued one first when
+        sync() was not called since the last submit)."""
+        if self._queued and not self._synced_since_submit:
+            self.sync()
+        sizes = self._last_sizes
         total = int(sizes.sum())
         buf = np.empty(max(total, 1), np.uint8)
         check(self._L.mjg_fetch(self._h, C.c_void_p(buf.ctypes.data), buf.size))

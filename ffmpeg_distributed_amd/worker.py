@@ -215,12 +215,15 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)
 
-    # two page-locked batches: the reader fills one while the GPU encodes the other
+    # three page-locked batches: the reader fills one while two are queued on the GPU (the
+    # encoder takes a second submit before the first is synced, so its kernels run back to
+    # back); a batch returns to the reader once its submit is synced.
     fb = enc.frame_bytes
-    bufs = [PinnedBuffer(BATCH * fb) for _ in range(2)]
+    nbuf = 3
+    bufs = [PinnedBuffer(BATCH * fb) for _ in range(nbuf)]
     free: "queue.Queue[int]" = queue.Queue()
     full: "queue.Queue" = queue.Queue()
-    for i in range(2):
+    for i in range(nbuf):
         free.put(i)
 
     def reader():
@@ -240,6 +243,19 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     th = threading.Thread(target=reader, daemon=True)
     th.start()
     frames = 0
+    queued: "list" = []  # buffer index and frame count per submit, oldest first
+
+    def drain_one():
+        nonlocal frames
+        j, m = queued.pop(0)
+        enc.sync()
+        packets = enc.fetch()
+        free.put(j)
+        for p in packets:
+            mkv.write_frame(p)
+        frames += m
+        prog.update(frames, sum(len(p) for p in packets))
+
     try:
         while True:
             item = full.get()
@@ -249,15 +265,14 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
                 raise item
             i, n = item
             if n:
+                if len(queued) == 2:
+                    drain_one()
                 enc.submit(bufs[i].array[: n * fb], n)
-                packets = enc.fetch()
-                free.put(i)
-                for p in packets:
-                    mkv.write_frame(p)
-                frames += n
-                prog.update(frames, sum(len(p) for p in packets))
+                queued.append((i, n))
             else:
                 free.put(i)
+        while queued:
+            drain_one()
         mkv.close()
         prog.update(frames, 0, final=True)
     finally:

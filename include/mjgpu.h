@@ -58,6 +58,10 @@ extern "C" {
 #define MJG_CHROMA_422 1       /* yuv(j)422p: MCU 16x16, Y 2x2 Cb 1x2 Cr 1x2 */
 #define MJG_CHROMA_444 2       /* yuv(j)444p: MCU 8x16, every component 1x2 (ff_mjpeg_init_hvsample) */
 
+#define MJG_F_TIMING_DETAIL 64u /* MJG_F_TIMING plus events around every tail kernel (scan, 0xFF
+                                  count, write: MJG_K_SCAN_BITS .. MJG_K_WRITE); each event adds
+                                  ~10 us of GPU idle between those short kernels */
+
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane)        */
 #define MJG_K_ENCODE 1         /* load + FDCT + quant + Huffman -> per-chunk bits     */
@@ -66,7 +70,8 @@ extern "C" {
 #define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes        */
 #define MJG_K_WRITE 5          /* header + stuffed scan + EOI into packed output     */
 #define MJG_K_HUFF 6           /* -huffman optimal: symbol-count pass + table build   */
-#define MJG_NUM_KERNELS 7
+#define MJG_K_TAIL 7           /* MJG_K_SCAN_BITS .. MJG_K_WRITE as one interval (MJG_F_TIMING) */
+#define MJG_NUM_KERNELS 8
 
 typedef struct mjg_config {
   int32_t src_w, src_h;      /* decoded frame size (packed I420: Y, then U, then V)    */
@@ -103,16 +108,19 @@ size_t mjg_frame_bytes(const mjg_ctx *ctx);
 int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 
 /* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously on the ctx
- * stream.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
+ * stream.  Up to two submits may be queued: the second one's kernels run right after the
+ * first's (each has its own output and scratch buffers); MJG_E_STATE with two queued.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
  * staging buffer; pinned memory from mjg_host_alloc() makes this asynchronous);
  * src_is_device = 1: `frames` is device memory on ctx's device, read in place.
  * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
 int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
-/* Wait for the last submit.  frame_sizes (may be NULL) receives nframes JPEG sizes;
- * *total (may be NULL) the packed total.  Grows the output buffer and re-runs the
- * final kernel if the packed output exceeded its capacity. */
+/* Wait for the oldest queued submit (with none queued: report the last synced one again).
+ * frame_sizes (may be NULL) receives its nframes JPEG sizes; *total (may be NULL) the packed
+ * total.  Grows the output buffer and re-runs the final kernel if the packed output
+ * exceeded its capacity. */
 int mjg_sync(mjg_ctx *ctx, uint64_t *frame_sizes, uint64_t *total);
-/* Copy the packed JPEGs of the last submit (frame after frame) to host memory. */
+/* Copy the packed JPEGs of the last synced submit (frame after frame) to host memory; syncs
+ * the oldest queued submit first when mjg_sync was not called since the last mjg_submit. */
 int mjg_fetch(mjg_ctx *ctx, uint8_t *out, size_t cap);
 /* Device pointers of the packed output and of the per-frame byte offsets (nframes+1
  * entries, valid after mjg_sync). */

@@ -306,3 +306,38 @@ def test_rst_with_optimal_is_rejected():
     from ffmpeg_distributed_amd._lib import MjgError
     with pytest.raises(MjgError):
         MjpegEncoder(0, 64, 64, huffman="optimal", rst=True)
+
+
+def test_pipelined_submits():
+    """Two submits queued at once (their kernels run back to back on the ctx stream, each
+    with its own scratch/output slot); sync completes them oldest first; a third queued
+    submit is refused; overflow regrowth works on a queued slot."""
+    from ffmpeg_distributed_amd._lib import MjgError
+    w, h, q = 96, 64, 4
+    frames = rand_frames(w, h, 7, seed=21, kind="smooth")
+    ref = oracle_frames(frames, w, h, q, False)
+    with MjpegEncoder(0, w, h, qscale=q, max_batch=3) as enc:
+        enc.submit(frames[0:3])
+        enc.submit(frames[3:5])
+        with pytest.raises(MjgError):
+            enc.submit(frames[5:7])
+        s0 = enc.sync()
+        got0 = enc.fetch()
+        enc.submit(frames[5:7])
+        s1 = enc.sync()
+        got1 = enc.fetch()
+        enc.sync()
+        got2 = enc.fetch()
+    assert got0 == ref[0:3] and list(s0) == [len(x) for x in ref[0:3]]
+    assert got1 == ref[3:5] and list(s1) == [len(x) for x in ref[3:5]]
+    assert got2 == ref[5:7]
+    # noise at q=2 overflows the packed output: regrow while the other slot is queued
+    nz = rand_frames(256, 128, 4, seed=5, kind="noise")
+    with MjpegEncoder(0, 256, 128, qscale=2, full_range=True, max_batch=2) as enc:
+        enc.submit(nz[:2])
+        enc.submit(nz[2:])
+        enc.sync()
+        a = enc.fetch()
+        enc.sync()
+        b = enc.fetch()
+    assert a + b == oracle_frames(nz, 256, 128, 2, True)
