@@ -153,9 +153,12 @@ struct PlaneScale {
 };
 
 // Per-submit state.  A context has two slots so a second mjg_submit can be queued before
-// the first is synced (the kernels of both run back to back on the ctx stream); everything
-// a submit's results and its overflow re-write need lives in its slot.  Slot 1 is
-// allocated on the first pipelined submit.
+// the first is synced; everything a submit's results and its overflow re-write need lives
+// in its slot.  Slot 1 is allocated on the first pipelined submit.  Two streams: the ctx
+// stream runs H2D, scale and k_encode; the tail stream runs a submit's scan/stuff/write
+// kernels after its k_encode (event enc_done), so the latency-bound tail of submit A runs
+// beside the VALU-bound k_encode of submit B.  A slot is reused only after the host synced
+// its previous submit (mjg_sync waits for `done`), so no device-side wait guards it.
 struct Slot {
   bool alloc = false, pending = false;
   int n = 0;
@@ -163,6 +166,7 @@ struct Slot {
   uint32_t *d_scratch = nullptr;
   uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
   uint32_t *d_frame_bits = nullptr, *d_status = nullptr;
+  uint32_t *d_work = nullptr;  // k_encode's batch counter (zero; reset by the slot's scan kernel)
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
   uint64_t *d_seg_size = nullptr;  // RST mode: stuffed segment sizes and offsets after the header
   uint32_t *d_seg_off = nullptr;
@@ -173,7 +177,7 @@ struct Slot {
   int16_t *d_dbg = nullptr;
   uint64_t *h_sizes = nullptr;
   uint32_t *h_status = nullptr;
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr, enc_done = nullptr;
   hipEvent_t ev[MJG_NUM_KERNELS][2] = {};
 };
 
@@ -182,7 +186,8 @@ struct Slot {
 struct mjg_ctx {
   int device = 0;
   mjg_config cfg{};
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // H2D, scale, k_encode
+  hipStream_t tail = nullptr;    // scans, stuffing, write, D2H of the sizes
   EncGeom geom{};
   int32_t qmat[64];
   int enc_grid = 0;
@@ -194,7 +199,6 @@ struct mjg_ctx {
   uint32_t *d_tabs = nullptr;
   uint8_t *d_hdr = nullptr;
   uint8_t *d_stage = nullptr, *d_scaled = nullptr;
-  uint32_t *d_work = nullptr;  // k_encode's batch counter (reset by the scan kernels)
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
@@ -218,13 +222,14 @@ void free_ctx(mjg_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_work, c->ps[0].hcp,
+  if (c->tail) (void)hipStreamSynchronize(c->tail);
+  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
                   c->ps[1].vps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
-    void *sp[] = {S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+    void *sp[] = {S.d_scratch, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
                   S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_out,
                   S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg};
     for (void *p : sp)
@@ -232,12 +237,14 @@ void free_ctx(mjg_ctx *c) {
     if (S.h_sizes) (void)hipHostFree(S.h_sizes);
     if (S.h_status) (void)hipHostFree(S.h_status);
     if (S.done) (void)hipEventDestroy(S.done);
+    if (S.enc_done) (void)hipEventDestroy(S.enc_done);
     for (auto &e : S.ev) {
       if (e[0]) (void)hipEventDestroy(e[0]);
       if (e[1]) (void)hipEventDestroy(e[1]);
     }
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->tail) (void)hipStreamDestroy(c->tail);
   delete c;
 }
 
@@ -315,8 +322,10 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
       (rc = dmalloc(&S.d_chunk_bits, B * NC)) || (rc = dmalloc(&S.d_chunk_off, B * NC)) ||
       (rc = dmalloc(&S.d_group_ff, B * NC)) || (rc = dmalloc(&S.d_ff_off, B * NC)) ||
       (rc = dmalloc(&S.d_frame_bits, B * NS)) || (rc = dmalloc(&S.d_status, 4)) ||
-      (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)))
+      (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)) ||
+      (rc = dmalloc(&S.d_work, 1)))
     return rc;
+  HIP_TRY(hipMemset(S.d_work, 0, sizeof(uint32_t)));
   if (c->rst && ((rc = dmalloc(&S.d_seg_size, B * NS)) || (rc = dmalloc(&S.d_seg_off, B * NS)))) return rc;
   S.out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096 + 2 * NS);
   if ((rc = dmalloc(&S.d_out, S.out_cap))) return rc;
@@ -332,6 +341,7 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   HIP_TRY(hipHostMalloc((void **)&S.h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void **)&S.h_status, 16, hipHostMallocDefault));
   HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&S.enc_done, hipEventDisableTiming));
   if (c->timing)
     for (auto &e : S.ev) {
       HIP_TRY(hipEventCreate(&e[0]));
@@ -363,6 +373,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   if (device < 0 || device >= ndev) return set_err(MJG_E_INVALID, "device %d of %d", device, ndev);
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));
 
   c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
   const int cf = k.chroma_format;
@@ -488,9 +499,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
 
   const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
   int rc;
-  if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size())) ||
-      (rc = dmalloc(&c->d_work, 1)))
-    return rc;
+  if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size()))) return rc;
   c->slot_B = B;
   c->slot_NC = NC;
   c->slot_NS = NS;
@@ -499,7 +508,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   if ((rc = alloc_slot(c, c->slot[0]))) return rc;
   if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
   HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(c->d_work, 0, sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
 
   if (c->scale) {
@@ -537,31 +545,31 @@ void tmark(mjg_ctx *c, Slot &S, int k, int end) {
   if (!c->timing) return;
   const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
   if (tail && !c->timing_detail) return;
-  (void)hipEventRecord(S.ev[k][end], c->stream);
+  (void)hipEventRecord(S.ev[k][end], tail ? c->tail : c->stream);
 }
 
 // status: reset the overflow flag first (the regrow path; a submit's scan kernel resets it)
 int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
   const EncGeom &g = c->geom;
   const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n * g.nseg;
-  if (reset_status) HIP_TRY(hipMemsetAsync(S.d_status, 0, 4, c->stream));
+  if (reset_status) HIP_TRY(hipMemsetAsync(S.d_status, 0, 4, c->tail));
   tmark(c, S, MJG_K_WRITE, 0);
-  k_frame_hdr<<<n, 64, 0, c->stream>>>(S.d_frame_size, c->d_hdr, (int)c->hdr.size(), S.d_out,
+  k_frame_hdr<<<n, 64, 0, c->tail>>>(S.d_frame_size, c->d_hdr, (int)c->hdr.size(), S.d_out,
                                        (uint64_t)S.out_cap, S.d_frame_offsets, S.d_status,
                                        c->optimal ? S.d_hdr_lens : nullptr, (int)c->dht_pos,
                                        (int)c->dht_end, S.d_dht, S.d_dht_nval, S.d_seg_off,
                                        S.d_seg_size, g.nseg);
-  k_write<<<(ngroups + 3) / 4, 256, 0, c->stream>>>(
+  k_write<<<(ngroups + 3) / 4, 256, 0, c->tail>>>(
       S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, S.d_ff_off, S.d_frame_size,
       S.d_frame_offsets, (int)c->hdr.size(), c->optimal ? S.d_hdr_lens : nullptr, g.nchunks, gpf,
       ngroups, S.d_out, (uint64_t)S.out_cap, S.d_seg_off, g.nseg);
   tmark(c, S, MJG_K_WRITE, 1);
-  if (c->timing && !c->timing_detail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->stream);
+  if (c->timing && !c->timing_detail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->tail);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(S.h_sizes, S.d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                         c->stream));
-  HIP_TRY(hipMemcpyAsync(S.h_status, S.d_status, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipEventRecord(S.done, c->stream));
+                         c->tail));
+  HIP_TRY(hipMemcpyAsync(S.h_status, S.d_status, 4, hipMemcpyDeviceToHost, c->tail));
+  HIP_TRY(hipEventRecord(S.done, c->tail));
   return MJG_OK;
 }
 
@@ -570,11 +578,11 @@ void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntas
   const EncGeom &g = c->geom;
   if (g.range_convert)
     k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
-        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, c->d_work, ntasks, S.d_hist,
+        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         S.d_ftabs);
   else
     k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
-        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, c->d_work, ntasks, S.d_hist,
+        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         S.d_ftabs);
 }
 
@@ -676,7 +684,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     tmark(c, S, MJG_K_HUFF, 0);
     HIP_TRY(hipMemsetAsync(S.d_hist, 0, (size_t)n * kFrameTabWords * 4, c->stream));
     launch_encode<kCount>(c, S, enc_in, wgs, ntasks);
-    HIP_TRY(hipMemsetAsync(c->d_work, 0, 4, c->stream));  // batch counter for pass 2
+    HIP_TRY(hipMemsetAsync(S.d_work, 0, 4, c->stream));  // batch counter for pass 2
     k_huff_build<<<n * 4, 64, 0, c->stream>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
     tmark(c, S, MJG_K_HUFF, 1);
     HIP_TRY(hipGetLastError());
@@ -688,19 +696,21 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     launch_encode<kEmitDefault>(c, S, enc_in, wgs, ntasks);
   tmark(c, S, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
-  if (c->timing && !c->timing_detail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->stream);
+  HIP_TRY(hipEventRecord(S.enc_done, c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->tail, S.enc_done, 0));
+  if (c->timing && !c->timing_detail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->tail);
   tmark(c, S, MJG_K_SCAN_BITS, 0);
   if (c->rst)
-    k_scan_bits_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits,
-                                                            g.nchunks, nsegs, c->d_work, S.d_status);
+    k_scan_bits_seg<<<(nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits,
+                                                            g.nchunks, nsegs, S.d_work, S.d_status);
   else
-    k_scan_bits<<<n, 1024, 0, c->stream>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, g.nchunks,
-                                           c->d_work, S.d_status);
+    k_scan_bits<<<n, 1024, 0, c->tail>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, g.nchunks,
+                                           S.d_work, S.d_status);
   tmark(c, S, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, S, MJG_K_COUNT_FF, 0);
   const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
-  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->stream>>>(S.d_scratch, S.d_chunk_bits, S.d_chunk_off,
+  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_scratch, S.d_chunk_bits, S.d_chunk_off,
                                                            S.d_frame_bits, S.d_group_ff, g.nchunks,
                                                            gpf, gpf * nsegs);
   tmark(c, S, MJG_K_COUNT_FF, 1);
@@ -708,12 +718,12 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   tmark(c, S, MJG_K_SCAN_FF, 0);
   // optimal: header = default header - its 348 table values + the frame's
   if (c->rst) {  // segment sizes (each with its RSTn / EOI trailer), then per-frame offsets
-    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->stream>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits,
                                                           S.d_seg_size, gpf, nsegs);
-    k_seg_sizes<<<n, 64, 0, c->stream>>>(S.d_seg_size, g.nseg, (int)c->hdr.size(), S.d_seg_off,
+    k_seg_sizes<<<n, 64, 0, c->tail>>>(S.d_seg_size, g.nseg, (int)c->hdr.size(), S.d_seg_off,
                                          S.d_frame_size);
   } else {
-    k_scan_ff<<<n, 1024, 0, c->stream>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, S.d_frame_size,
+    k_scan_ff<<<n, 1024, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, S.d_frame_size,
                                          gpf, (int)c->hdr.size(), c->optimal ? S.d_dht_nval : nullptr,
                                          (int)c->hdr.size() - 348, S.d_hdr_lens);
   }
@@ -915,6 +925,7 @@ int mjg_debug_filter(mjg_ctx *c, int plane, int dir, int16_t *coeff, int32_t *po
 #ifdef MJG_STAMPS
 extern "C" int mjg_debug_stamps(mjg_ctx *c, uint64_t *out, size_t n) {
   HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->tail));
   HIP_TRY(hipMemcpy(out, c->slot[0].d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return MJG_OK;
 }

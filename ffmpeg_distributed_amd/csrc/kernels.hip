@@ -1199,39 +1199,90 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
   if (lane == 0) seg_bits[sg] = t;
 }
 
-// Word k (32 bits, MSB first) of frame f's unstuffed scan, for a word owned by chunk c
-// (its first bit lies in chunk c).  Bits past the chunk come from chunk c+1, or for the
-// frame's last chunk are the 1-bit padding to a byte boundary (ff_mjpeg_escape_FF pad).
-__device__ __forceinline__ uint32_t chunk_bits_at(const uint32_t *slot, uint32_t p, uint32_t len) {
-  const uint32_t wi = p >> 5, s = p & 31;
-  const uint32_t nw = (len + 31) >> 5;
-  uint32_t v = slot[wi];
-  if (s) {
-    const uint32_t w1 = (wi + 1 < nw) ? slot[wi + 1] : 0u;
-    v = (v << s) | (w1 >> (32 - s));
-  }
-  const uint32_t rem = len - p;
-  if (rem < 32) v &= ~(0xffffffffu >> rem);
-  return v;
+// Realign/stuff kernels work on *groups* of kChunksPerWave consecutive chunks of an
+// entropy-coded segment (the frame unless RST mode), one wave per group, lanes = the group's
+// words flattened across its chunks.  A word belongs to the chunk holding its first bit, so
+// chunk c owns words [ceil(O_c / 32), ceil(O_{c+1} / 32)) and a group owns one contiguous
+// word range.  Everything per group (offsets, lengths) lives in lane registers, so a word
+// costs only its slot loads, and a round issues all of them before any is used: the kernels
+// are load-latency bound (one wave per ~200 words), not bandwidth bound.
+constexpr int kChunksPerWave = 8;
+constexpr int kWordsPerLane = 4;  // words per lane per round
+
+struct GroupWords {
+  int f, c0, n;          // segment, first chunk, chunks in the group
+  uint32_t T, total_bytes;
+  uint32_t k0, k1;       // owned word range
+  uint32_t o_lane;       // lane j < n: O_{c0+j}; lane n: end offset of the group
+  uint32_t l_lane;       // lane j <= n: L_{c0+j} (lane n: the next group's first chunk, 0 past the segment)
+  const uint32_t *slot0; // scratch slot of chunk c0
+  int nchunks;
+};
+
+__device__ __forceinline__ GroupWords group_words(const uint32_t *scratch, const uint32_t *chunk_bits,
+                                                  const uint32_t *chunk_off, const uint32_t *frame_bits,
+                                                  int nchunks, int ngroups_per_frame, int gi, int lane) {
+  GroupWords g;
+  g.f = gi / ngroups_per_frame;
+  g.c0 = (gi - g.f * ngroups_per_frame) * kChunksPerWave;
+  g.n = min(kChunksPerWave, nchunks - g.c0);
+  g.nchunks = nchunks;
+  g.T = frame_bits[g.f];
+  g.total_bytes = (g.T + 7) >> 3;
+  const size_t i0 = (size_t)g.f * nchunks + g.c0;
+  g.slot0 = scratch + i0 * kSlotWords;
+  g.o_lane = lane < g.n ? chunk_off[i0 + lane] : 0u;
+  g.l_lane = (lane <= g.n && g.c0 + lane < nchunks) ? chunk_bits[i0 + lane] : 0u;
+  const uint32_t last = __shfl(g.o_lane, g.n - 1, 64) + __shfl(g.l_lane, g.n - 1, 64);
+  if (lane == g.n) g.o_lane = last;
+  g.k0 = (__shfl(g.o_lane, 0, 64) + 31) >> 5;
+  g.k1 = (last + 31) >> 5;
+  return g;
 }
 
-__device__ __forceinline__ uint32_t aligned_word(const uint32_t *scratch, const uint32_t *cbits,
-                                                 int nchunks, int f, int c, uint32_t O, uint32_t L,
-                                                 uint32_t T, uint32_t k) {
-  const uint32_t *slot = scratch + ((size_t)f * nchunks + c) * kSlotWords;
-  const uint32_t p = 32 * k - O;
-  uint32_t v = chunk_bits_at(slot, p, L);
-  const uint32_t rem = L - p;
+// Word k (32 bits, MSB first) of the segment's unstuffed scan, in two steps so a caller can
+// issue the loads of several words before using any: word_load finds the owner chunk c
+// (relative to the group; uniform readlane compares) and loads the three slot words the
+// word can need (independent, unconditional loads), word_value assembles it.  Bits past the
+// chunk come from chunk c+1's first word, or for the segment's last chunk are the 1-bit
+// padding to a byte boundary (ff_mjpeg_escape_FF pad).  k must lie in [k0, k1).
+struct WordLoad {
+  uint32_t w0, w1, w2, L, NL, p;
+  bool has_next;
+};
+
+__device__ __forceinline__ WordLoad word_load(const GroupWords &g, uint32_t k) {
+  int c = 0;
+#pragma unroll
+  for (int j = 1; j < kChunksPerWave; j++) {
+    const uint32_t oj = __builtin_amdgcn_readlane(g.o_lane, j);
+    c += (j < g.n && k >= ((oj + 31) >> 5)) ? 1 : 0;
+  }
+  WordLoad r;
+  const uint32_t O = __shfl(g.o_lane, c, 64);
+  r.L = __shfl(g.l_lane, c, 64);
+  r.NL = __shfl(g.l_lane, c + 1, 64);
+  r.p = 32 * k - O;
+  r.has_next = g.c0 + c + 1 < g.nchunks;
+  const uint32_t *slot = g.slot0 + (size_t)c * kSlotWords;
+  const uint32_t wi = r.p >> 5;
+  r.w0 = slot[wi];
+  r.w1 = slot[min(wi + 1, (uint32_t)kSlotWords - 1)];  // clamped into the slot
+  r.w2 = slot[r.has_next ? kSlotWords : 0];            // next chunk's first word
+  return r;
+}
+
+__device__ __forceinline__ uint32_t word_value(const GroupWords &g, const WordLoad &r) {
+  const uint32_t wi = r.p >> 5, s = r.p & 31, nw = (r.L + 31) >> 5;
+  const uint32_t w1 = wi + 1 < nw ? r.w1 : 0u;
+  uint32_t v = s ? (r.w0 << s) | (w1 >> (32 - s)) : r.w0;
+  const uint32_t rem = r.L - r.p;  // > 0: the word's first bit lies in its chunk
   if (rem < 32) {
-    if (c + 1 < nchunks) {
-      const uint32_t *nslot = slot + kSlotWords;
-      const uint32_t nl = cbits[(size_t)f * nchunks + c + 1];
-      v |= chunk_bits_at(nslot, 0, nl) >> rem;
-    } else {
-      const uint32_t pad = (8 - (T & 7)) & 7;
-      const uint32_t ones = (0xffffffffu >> rem) & ~(rem + pad >= 32 ? 0u : (0xffffffffu >> (rem + pad)));
-      v |= ones;
-    }
+    v &= ~(0xffffffffu >> rem);
+    const uint32_t nv = r.NL < 32 ? r.w2 & ~(0xffffffffu >> r.NL) : r.w2;
+    const uint32_t pad = (8 - (g.T & 7)) & 7;
+    const uint32_t ones = (0xffffffffu >> rem) & ~(rem + pad >= 32 ? 0u : (0xffffffffu >> (rem + pad)));
+    v |= r.has_next ? nv >> rem : ones;
   }
   return v;
 }
@@ -1244,53 +1295,6 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
-// Realign/stuff kernels work on *groups* of kChunksPerWave consecutive chunks of a frame,
-// one wave per group, lanes = the group's words flattened across its chunks.  A word
-// belongs to the chunk holding its first bit, so chunk c owns words
-// [ceil(O_c / 32), ceil(O_{c+1} / 32)) and a group owns one contiguous word range.
-constexpr int kChunksPerWave = 8;
-
-struct GroupWords {
-  int f, c0, n;          // frame, first chunk, chunks in the group
-  uint32_t T, total_bytes;
-  uint32_t k0, k1;       // owned word range
-  uint32_t o_lane;       // lane j < n: O_{c0+j}; lane n: end offset of the group
-  const uint32_t *chunk_off, *chunk_bits;  // the group's first chunk
-};
-
-__device__ __forceinline__ GroupWords group_words(const uint32_t *chunk_bits, const uint32_t *chunk_off,
-                                                  const uint32_t *frame_bits, int nchunks,
-                                                  int ngroups_per_frame, int gi, int lane) {
-  GroupWords g;
-  g.f = gi / ngroups_per_frame;
-  g.c0 = (gi - g.f * ngroups_per_frame) * kChunksPerWave;
-  g.n = min(kChunksPerWave, nchunks - g.c0);
-  g.T = frame_bits[g.f];
-  g.total_bytes = (g.T + 7) >> 3;
-  const size_t i0 = (size_t)g.f * nchunks + g.c0;
-  g.chunk_off = chunk_off + i0;
-  g.chunk_bits = chunk_bits + i0;
-  g.o_lane = lane < g.n ? chunk_off[i0 + lane] : 0u;
-  const uint32_t last = __shfl(g.o_lane, g.n - 1, 64) + chunk_bits[i0 + g.n - 1];
-  if (lane == g.n) g.o_lane = last;
-  g.k0 = (__shfl(g.o_lane, 0, 64) + 31) >> 5;
-  g.k1 = (last + 31) >> 5;
-  return g;
-}
-
-// Owner chunk (relative to the group) of word k, its offset O and length L.
-__device__ __forceinline__ int word_owner(const GroupWords &g, uint32_t k, uint32_t &O, uint32_t &L) {
-  int c = 0;
-#pragma unroll
-  for (int j = 1; j < kChunksPerWave; j++) {
-    const uint32_t oj = __builtin_amdgcn_readlane(g.o_lane, j);
-    c += (j < g.n && k >= ((oj + 31) >> 5)) ? 1 : 0;
-  }
-  O = g.chunk_off[c];
-  L = g.chunk_bits[c];
-  return c;
-}
-
 __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
                                                   const uint32_t *__restrict__ chunk_bits,
                                                   const uint32_t *__restrict__ chunk_off,
@@ -1299,13 +1303,21 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
                                                   int ngroups_per_frame, int ngroups) {
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (gi >= ngroups) return;
-  const GroupWords g = group_words(chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
+  const GroupWords g =
+      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
   int cnt = 0;
-  for (uint32_t k = g.k0 + lane; k < g.k1; k += 64) {
-    uint32_t O, L;
-    const int c = word_owner(g, k, O, L);
-    cnt += ff_in_word(aligned_word(scratch, chunk_bits, nchunks, g.f, g.c0 + c, O, L, g.T, k), 4 * k,
-                      g.total_bytes);
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
+    WordLoad ld[kWordsPerLane];
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
+    uint32_t v[kWordsPerLane];
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i]);
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) {
+      const uint32_t k = kb + 64 * i + lane;
+      if (k < g.k1) cnt += ff_in_word(v[i], 4 * k, g.total_bytes);
+    }
   }
   cnt = wave_sum(cnt);
   if (lane == 0) group_ff[gi] = (uint32_t)cnt;
@@ -1447,35 +1459,43 @@ __global__ __launch_bounds__(256) void k_write(
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (gi >= ngroups) return;
   // g.f is the entropy-coded segment (the frame itself unless RST mode)
-  const GroupWords g = group_words(chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
+  const GroupWords g =
+      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
   const int fr = g.f / nseg;
   const uint64_t foff = frame_offsets[fr];
   if (foff + frame_size[fr] > out_cap) return;  // k_frame_hdr flagged the overflow
   const uint32_t hl = hdr_lens ? hdr_lens[fr] : (uint32_t)hdr_len;
   uint8_t *base = out + foff + hl + (seg_off ? seg_off[g.f] : 0u) + 4 * (size_t)g.k0 + ff_off[gi];
   uint32_t carry = 0;
-  for (uint32_t kb = g.k0; kb < g.k1; kb += 64) {
-    const uint32_t k = kb + lane;
-    uint32_t v = 0, cnt = 0;
-    if (k < g.k1) {
-      uint32_t O, L;
-      const int c = word_owner(g, k, O, L);
-      v = aligned_word(scratch, chunk_bits, nchunks, g.f, g.c0 + c, O, L, g.T, k);
-      cnt = (uint32_t)ff_in_word(v, 4 * k, g.total_bytes);
-    }
-    const uint32_t incl = wave_incl_scan(cnt, lane);
-    if (k < g.k1) {
-      uint8_t *p = base + 4 * (k - g.k0) + carry + incl - cnt;
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
+    WordLoad ld[kWordsPerLane];
 #pragma unroll
-      for (int bb = 0; bb < 4; bb++) {
-        if (4 * k + bb < g.total_bytes) {
-          const uint8_t byte = (uint8_t)(v >> (24 - 8 * bb));
-          *p++ = byte;
-          if (byte == 0xff) *p++ = 0;
+    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
+    uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i]);
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) {
+      const uint32_t k = kb + 64 * i + lane;
+      cnt[i] = k < g.k1 ? (uint32_t)ff_in_word(v[i], 4 * k, g.total_bytes) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) {
+      const uint32_t k = kb + 64 * i + lane;
+      const uint32_t incl = wave_incl_scan(cnt[i], lane);
+      if (k < g.k1) {
+        uint8_t *p = base + 4 * (k - g.k0) + carry + incl - cnt[i];
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+          if (4 * k + bb < g.total_bytes) {
+            const uint8_t byte = (uint8_t)(v[i] >> (24 - 8 * bb));
+            *p++ = byte;
+            if (byte == 0xff) *p++ = 0;
+          }
         }
       }
+      carry += __shfl(incl, 63, 64);
     }
-    carry += __shfl(incl, 63, 64);
   }
 }
 

@@ -135,7 +135,7 @@ class MjpegEncoder:
     def submit(self, frames=None, nframes: Optional[int] = None, device_ptr: Optional[int] = None):
         """Queue `nframes` packed frames: a host buffer (numpy / bytes) or a device pointer
         (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU).  Two submits may be queued;
-        their kernels run back to back on the context's stream."""
+        the second's k_encode runs beside the first's tail kernels (two streams)."""
         if device_ptr is not None:
             if nframes is None:
                 raise ValueError("nframes is required with device_ptr")

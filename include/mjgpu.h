@@ -107,9 +107,11 @@ size_t mjg_frame_bytes(const mjg_ctx *ctx);
  * default tables (same layout, different DHT contents). */
 int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 
-/* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously on the ctx
- * stream.  Up to two submits may be queued: the second one's kernels run right after the
- * first's (each has its own output and scratch buffers); MJG_E_STATE with two queued.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
+/* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously: H2D, scale and
+ * k_encode on the ctx stream, the scan/stuff/write tail on the ctx's second (tail) stream
+ * after the submit's k_encode.  Up to two submits may be queued: the second one's k_encode
+ * runs beside the first's tail (each has its own output and scratch buffers); MJG_E_STATE
+ * with two queued.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
  * staging buffer; pinned memory from mjg_host_alloc() makes this asynchronous);
  * src_is_device = 1: `frames` is device memory on ctx's device, read in place.
  * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
@@ -125,7 +127,8 @@ int mjg_fetch(mjg_ctx *ctx, uint8_t *out, size_t cap);
 /* Device pointers of the packed output and of the per-frame byte offsets (nframes+1
  * entries, valid after mjg_sync). */
 int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offsets);
-/* The hipStream_t the context launches on (for event timing by the caller). */
+/* The hipStream_t the context launches H2D, scale and k_encode on (for event timing by the
+ * caller; the tail kernels run on a second stream ordered after k_encode). */
 void *mjg_stream(mjg_ctx *ctx);
 
 /* Pinned host memory for mjg_submit / mjg_fetch. */
