@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -533,6 +534,8 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
+  if (const char *e = getenv("MJG_ENC_WG_PER_CU")) per_cu = atoi(e);  // perf experiments
+  if (getenv("MJG_DEBUG_GRID")) fprintf(stderr, "mjg: %d CUs, %d k_encode workgroups per CU\n", ncu, per_cu);
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
 
   return MJG_OK;

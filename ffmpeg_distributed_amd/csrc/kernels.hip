@@ -30,9 +30,14 @@
 #ifndef MJG_RC_LUT
 #define MJG_RC_LUT 1  // tv->pc range conversion through a 512-byte LDS table (0: fp32 fma + med3)
 #endif
+#ifndef MJG_ROW_DOT2
+#define MJG_ROW_DOT2 0  // 1: row pass on packed int16 butterflies + v_dot2_i32_i16 (measured no faster: v_mov
+                        // for each biased accumulator, v_perm to pair the LDS table reads)
+#endif
 #ifndef MJG_ABLATE
 #define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store,
-                      // 5 candidates not quantised exactly (v = 1 or 2)
+                      // 5 candidates not quantised exactly (v = 1 or 2), 6 no zigzag scatter of the
+                      // candidate bits, 7 no long-block (> 128 bits) re-emission
 #endif
 
 namespace mjg {
@@ -291,6 +296,22 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
 // runs and EOB are those of the exact block.  (Mean nonzero AC per block is ~1.3 on
 // testsrc2 4K q5, so the loop is short.)
 template <class Sink>
+__device__ __forceinline__ void emit_ac(int k, int v, int &prev, Sink &sink) {
+  if (v == 0) return;  // screened in, quantises to zero
+  int run = k - prev - 1;
+  prev = k;
+  while (run >= 16) {
+    sink.ac(0xf0, 0, 0u);  // ZRL
+    run -= 16;
+  }
+  const int a = v < 0 ? -v : v;
+  const int cat = 32 - __clz(a);
+  sink.ac(((run & 15) << 4) | cat, cat, (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u));
+}
+
+// Candidates are taken two at a time so the LDS reads of both (zigzag -> natural index,
+// the column of the row image, the quantiser) are in flight together.
+template <class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
                                            const uint8_t *zz, const uint32_t *m2, const int *qc,
                                            Sink &sink) {
@@ -300,23 +321,19 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
   }
   int prev = 0;
   while (cand) {
-    const int k = (int)__builtin_ctzll(cand);
+    const int k1 = (int)__builtin_ctzll(cand);
     cand &= cand - 1;
+    const bool two = cand != 0;
+    const int k2 = two ? (int)__builtin_ctzll(cand) : k1;
+    cand &= cand - 1;  // no-op when cand == 0
 #if MJG_ABLATE == 5
-    const int v = 1 + (k & 1);
+    const int v1 = 1 + (k1 & 1), v2 = 1 + (k2 & 1);
 #else
-    const int v = exact_coef(pkcol, zz[k], m2, qc);
+    const int v1 = exact_coef(pkcol, zz[k1], m2, qc);
+    const int v2 = exact_coef(pkcol, zz[k2], m2, qc);
 #endif
-    if (v == 0) continue;  // screened in, quantises to zero
-    int run = k - prev - 1;
-    prev = k;
-    while (run >= 16) {
-      sink.ac(0xf0, 0, 0u);  // ZRL
-      run -= 16;
-    }
-    const int a = v < 0 ? -v : v;
-    const int cat = 32 - __clz(a);
-    sink.ac(((run & 15) << 4) | cat, cat, (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u));
+    emit_ac(k1, v1, prev, sink);
+    if (two) emit_ac(k2, v2, prev, sink);
   }
   if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB
 }
@@ -479,7 +496,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
-  __shared__ uint8_t s_rc[MJG_RC_LUT ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
+  __shared__ uint8_t s_rc[(MJG_RC_LUT || MJG_ROW_DOT2) ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
   __shared__ uint32_t s_skip[12];                  // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
@@ -501,7 +518,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_desc[tid] = tabs[672 + tid];
   }
   if (tid < 12) s_skip[tid] = tabs[680 + tid];
-  if (MJG_RC_LUT && RC)
+  if ((MJG_RC_LUT || MJG_ROW_DOT2) && RC)
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
   uint32_t *s_pk = s_pk_all[wave];
@@ -570,6 +587,61 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       for (int j = 0; j < 4; j++) s_pk[(r * 4 + j) * 64 + lane] = (uint32_t)(raw[r] >> (16 * (j & 1)));
     if (false)
 #endif
+#if MJG_ROW_DOT2
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      // Row pass (jfdctint pass 1) on packed int16 pairs, exactly: pixel pairs A = (p0, p1),
+      // B = (p7, p6), C = (p3, p2), D = (p4, p5) -- v_perm of the row bytes, or [RC] two LDS
+      // table reads into the halves of one register (swscale's tv->pc value per pixel, the
+      // address (tab << 8) | pixel built by one v_perm) -- then the butterfly sums and
+      // differences two at a time (v_pk_add/sub_u16; every value fits int16), and each
+      // output as one or two v_dot2_i32_i16 of (t7, t6), (t4, t5), (t13, t12) or (t10, t11)
+      // with the LLM constants multiplied out (the kPass2Dot rows).  The accumulator starts
+      // at DESCALE's 256 plus 32768 << 9, so the shift by 9 leaves value + 32768, the u16
+      // the row image stores; rows 0 / 4 (x16, no descale) start at 32768.
+      const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
+      u16x2 A, B, C, D;
+      if (rc) {
+        const uint8_t *lut = s_rc;
+        const uint32_t t8 = (uint32_t)tab;
+        A.x = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0400u)];
+        A.y = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0401u)];
+        B.x = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0403u)];
+        B.y = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0402u)];
+        C.x = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0403u)];
+        C.y = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0402u)];
+        D.x = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0400u)];
+        D.y = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0401u)];
+      } else {
+        A = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u));
+        B = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c060c07u));
+        C = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c020c03u));
+        D = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c050c04u));
+      }
+      const u16x2 s01 = A + B, d76 = A - B, s32 = C + D, d45 = C - D;  // (t0,t1) (t7,t6) (t3,t2) (t4,t5)
+      const short2_t e = __builtin_bit_cast(short2_t, s01 + s32);      // (t10, t11)
+      const short2_t f = __builtin_bit_cast(short2_t, s01 - s32);      // (t13, t12)
+      const short2_t o76 = __builtin_bit_cast(short2_t, d76), o45 = __builtin_bit_cast(short2_t, d45);
+      constexpr int kB = 256 + (32768 << 9);
+#define MJG_C2(a, b) (short2_t{(short)(a), (short)(b)})
+#define MJG_D2(x, c, acc) __builtin_amdgcn_sdot2((x), MJG_C2 c, (acc), false)
+      const uint32_t o0 = (uint32_t)MJG_D2(e, (16, 16), 32768);
+      const uint32_t o4 = (uint32_t)MJG_D2(e, (16, -16), 32768);
+      const uint32_t o2 = (uint32_t)MJG_D2(f, (10703, 4433), kB) >> 9;
+      const uint32_t o6 = (uint32_t)MJG_D2(f, (4433, -10704), kB) >> 9;
+      const uint32_t o1 = (uint32_t)MJG_D2(o76, (11363, 9633), MJG_D2(o45, (2260, 6437), kB)) >> 9;
+      const uint32_t o3 = (uint32_t)MJG_D2(o76, (9633, -2259), MJG_D2(o45, (-6436, -11362), kB)) >> 9;
+      const uint32_t o5 = (uint32_t)MJG_D2(o76, (6437, -11362), MJG_D2(o45, (9633, 2261), kB)) >> 9;
+      const uint32_t o7 = (uint32_t)MJG_D2(o76, (2260, -6436), MJG_D2(o45, (-11363, 9633), kB)) >> 9;
+#undef MJG_D2
+#undef MJG_C2
+      s_pk[(r * 4 + 0) * 64 + lane] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);
+      s_pk[(r * 4 + 1) * 64 + lane] = __builtin_amdgcn_perm(o3, o2, 0x05040100u);
+      s_pk[(r * 4 + 2) * 64 + lane] = __builtin_amdgcn_perm(o5, o4, 0x05040100u);
+      s_pk[(r * 4 + 3) * 64 + lane] = __builtin_amdgcn_perm(o7, o6, 0x05040100u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < 8; r++) {
       const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
@@ -631,6 +703,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
             __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     // prefetch the next chunk while this one is encoded
     const int cur_frame = frame, cur_chunk = chunk, cur_bbase = bbase;
     const bool cur_active = active;
@@ -753,6 +826,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     }
     // candidate bits -> zigzag-ordered mask (a handful of candidates per block)
     uint64_t mask = 0;
+#if MJG_ABLATE == 6
+    mask = ((uint64_t)cb << 32) | (ca << 1);
+    ca = cb = 0;
+#endif
     while (ca) {
       const int pos = __builtin_ctz(ca);
       ca &= ca - 1;
@@ -808,7 +885,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     ShiftSink q;
     q.act = act;
     q.dct = dct;
-#if MJG_ABLATE == 0 || MJG_ABLATE == 4
+#if MJG_ABLATE == 0 || MJG_ABLATE >= 4
     if (cur_active) {
       emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
       q.finish();
@@ -834,7 +911,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const uint32_t lw = has ? (off + q.bits - 1) >> 5 : fw;
     uint32_t head = 0, tail = 0;
     if (has && MJG_ABLATE != 4) {
-      if (q.bits <= 128) {
+      if (q.bits <= 128 || MJG_ABLATE == 7) {
         // the block's words from its end: d[4] = word lw, d[4 - j] = word lw - j, i.e. the
         // right-aligned 128 bits shifted left by t, the free bits after the block in word lw
         const uint32_t t = (32u - ((off + q.bits) & 31u)) & 31u, sh = 32u - t;  // sh in 1..32
