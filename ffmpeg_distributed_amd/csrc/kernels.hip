@@ -37,7 +37,8 @@
 #ifndef MJG_ABLATE
 #define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store,
                       // 5 candidates not quantised exactly (v = 1 or 2), 6 no zigzag scatter of the
-                      // candidate bits, 7 no long-block (> 128 bits) re-emission
+                      // candidate bits, 7 no long-block (> 128 bits) re-emission, 8 at most 12
+                      // candidates per block
 #endif
 
 namespace mjg {
@@ -841,6 +842,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       mask |= 1ull << s_scat[32 + pos];
     }
 
+#if MJG_ABLATE == 8  // perf experiment: heavy blocks cut to their first 12 candidates
+    for (int i = __popcll(mask); i > 12; i--) mask &= ~(1ull << (63 - __clzll(mask)));
+#endif
     // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.
     const int delta = desc_delta(dsc);
