@@ -200,6 +200,7 @@ struct mjg_ctx {
   uint32_t *d_tabs = nullptr;
   uint8_t *d_hdr = nullptr;
   uint8_t *d_stage = nullptr, *d_scaled = nullptr;
+  uint32_t *d_stage_bits = nullptr;  // k_encode: per wave, lane-major staging of blocks past 128 bits
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
@@ -224,7 +225,7 @@ void free_ctx(mjg_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->tail) (void)hipStreamSynchronize(c->tail);
-  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->ps[0].hcp,
+  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_stage_bits, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
                   c->ps[1].vps};
   for (void *p : ptrs)
@@ -537,6 +538,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   if (const char *e = getenv("MJG_ENC_WG_PER_CU")) per_cu = atoi(e);  // perf experiments
   if (getenv("MJG_DEBUG_GRID")) fprintf(stderr, "mjg: %d CUs, %d k_encode workgroups per CU\n", ncu, per_cu);
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
+  {
+    const int rc2 = dmalloc(&c->d_stage_bits, (size_t)c->enc_grid * kWavesPerWg * 64 * kStageWords);
+    if (rc2) return rc2;
+  }
 
   return MJG_OK;
 }
@@ -582,11 +587,11 @@ void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntas
   if (g.range_convert)
     k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        S.d_ftabs);
+        S.d_ftabs, c->d_stage_bits);
   else
     k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        S.d_ftabs);
+        S.d_ftabs, c->d_stage_bits);
 }
 
 }  // namespace

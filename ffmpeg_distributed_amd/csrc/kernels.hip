@@ -203,53 +203,33 @@ __device__ __forceinline__ int wave_sum(int v) {
     emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);                        \
   }
 
-// Second emission pass of a block longer than RegSink's 4 words: bits at the block's
-// chunk offset, interior words stored to the slot, first/last word kept for the opener
-// logic of the pack step (k_encode).
-struct SlotSink {
-  MJG_SINK_SYMBOLS
-  uint64_t acc;
-  int nacc;          // bits held in acc (< 32 between emits)
-  uint32_t widx;     // chunk-relative index of the word being filled
-  uint32_t fw, lw;   // the block's first and last word
-  uint32_t *slot;
-  uint32_t head, tail;
-  __device__ __forceinline__ void put(uint32_t w) {
-    if (widx == fw)
-      head = w;
-    else if (widx == lw)
-      tail = w;
-    else
-      slot[widx] = w;
-    widx++;
-  }
-  __device__ __forceinline__ void emit(uint32_t v, int n) {
-    acc = (acc << n) | v;
-    nacc += n;
-    if (nacc >= 32) {
-      nacc -= 32;
-      put((uint32_t)(acc >> nacc));
-    }
-  }
-  __device__ __forceinline__ void finish() {
-    if (nacc > 0) put((uint32_t)(acc << (32 - nacc)));
-  }
-};
-
 __device__ __forceinline__ int dc_cat(int diff) {
   const int a = diff < 0 ? -diff : diff;
   return diff == 0 ? 0 : 32 - __clz(a);
 }
 
-// First emission pass: the block's last 128 bits right-aligned in a 4-register shift
-// register (w3 lowest; the block's offset in the chunk is not known yet), and the total bit
-// count (blocks over 128 bits are re-emitted by SlotSink).  Branch-free: appending n <= 26
-// bits is four funnel shifts, (w_i << n) | (w_i+1 >> (32 - n)), one v_alignbit each.
+// The emission pass: the block's last 128 bits right-aligned in a 4-register shift register
+// (w3 lowest; the block's offset in the chunk is not known yet), and the total bit count.
+// Appending n <= 26 bits is four funnel shifts, (w_i << n) | (w_i+1 >> (32 - n)), one
+// v_alignbit each.  A block longer than 128 bits (rare: text-like detail) spills its stream
+// word by word to the lane's staging column in HBM (stage[j * 64] = stream bits
+// [32j, 32j + 32)) just before the word would leave the window; flush() then writes the
+// rest, and the pack step copies the staged stream to its place in the slot.
 struct ShiftSink {
   MJG_SINK_SYMBOLS
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   uint32_t bits = 0;
+  uint32_t spilled = 0;  // stream bits already staged (multiple of 32); bits - spilled <= 128
+  uint32_t *stage;
+  // the staged word at stream bit `spilled`: window offset o = 128 - (bits - spilled) from the top
+  __device__ __forceinline__ uint32_t window_word(uint32_t o, uint32_t a, uint32_t b) const {
+    return o ? __builtin_amdgcn_alignbit(a, b, 32u - o) : a;
+  }
   __device__ __forceinline__ void emit(uint32_t v, int n) {
+    if (bits + (uint32_t)n - spilled > 128u) {  // the oldest unstaged word would be shifted out
+      stage[(spilled >> 5) * 64] = window_word(128u - (bits - spilled), w0, w1);
+      spilled += 32;
+    }
     const uint32_t sh = 32u - (uint32_t)n;
     w0 = __builtin_amdgcn_alignbit(w0, w1, sh);
     w1 = __builtin_amdgcn_alignbit(w1, w2, sh);
@@ -258,7 +238,18 @@ struct ShiftSink {
     bits += (uint32_t)n;
   }
   __device__ __forceinline__ void finish() {}
+  // a block past 128 bits: stage the words still in the window (stream words
+  // spilled/32 .. (bits-1)/32, at most 4)
+  __device__ __forceinline__ void flush() {
+    const uint32_t o = 128u - (bits - spilled), j0 = spilled >> 5, nrem = (bits - spilled + 31) >> 5;
+    stage[j0 * 64] = window_word(o, w0, w1);
+    if (nrem > 1) stage[(j0 + 1) * 64] = window_word(o, w1, w2);
+    if (nrem > 2) stage[(j0 + 2) * 64] = window_word(o, w2, w3);
+    if (nrem > 3) stage[(j0 + 3) * 64] = window_word(o, w3, 0u);
+  }
 };
+
+constexpr int kStageWords = (kMaxBlockBits + 31) / 32;  // staged words per lane
 
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
 // image (pkcol = s_pk + lane: word [r*4 + c/2] holds rows r, columns c, c+1 as u16 = value
@@ -489,7 +480,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
-    uint32_t *__restrict__ hist, const uint32_t *__restrict__ ftabs) {
+    uint32_t *__restrict__ hist, const uint32_t *__restrict__ ftabs, uint32_t *__restrict__ stage_all) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
@@ -889,10 +880,11 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     ShiftSink q;
     q.act = act;
     q.dct = dct;
+    q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
 #if MJG_ABLATE == 0 || MJG_ABLATE >= 4
     if (cur_active) {
       emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
-      q.finish();
+      if (q.bits > 128) q.flush();
     }
 #else
     if (cur_active) {
@@ -929,22 +921,25 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
         for (int j = 1; j < 4; j++)
           if ((uint32_t)j < nmid) slot[lw - j] = d[4 - j];
         head = nmid == 0 ? d[4] : nmid == 1 ? d[3] : nmid == 2 ? d[2] : nmid == 3 ? d[1] : d[0];
-      } else {  // long block: re-emit, interior words straight to the slot
-        SlotSink sink;
-        sink.act = act;
-        sink.dct = dct;
-        sink.acc = 0;
-        sink.nacc = (int)sft;
-        sink.widx = fw;
-        sink.fw = fw;
-        sink.lw = lw;
-        sink.slot = slot;
-        sink.head = 0;
-        sink.tail = 0;
-        emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, sink);
-        sink.finish();
-        head = sink.head;
-        tail = sink.tail;
+      } else {  // long block: its staged stream shifted into place, 8 words per step
+        const uint32_t nws = (q.bits + 31) >> 5, nw = lw - fw + 1;
+        const uint32_t *stg = q.stage;
+        for (uint32_t m0 = 0; m0 < nw; m0 += 8) {
+          uint32_t S[9];
+#pragma unroll
+          for (int i = 0; i < 9; i++) {  // stream words m0 - 1 .. m0 + 7 (0 outside the stream)
+            const uint32_t j = m0 - 1 + (uint32_t)i;
+            S[i] = j < nws ? stg[j * 64] : 0u;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const uint32_t m = m0 + (uint32_t)i;
+            const uint32_t F = sft ? (S[i] << (32u - sft)) | (S[i + 1] >> sft) : S[i + 1];
+            if (m == 0) head = F;
+            if (m + 1 == nw && m > 0) tail = F;
+            if (m > 0 && m + 1 < nw) slot[fw + m] = F;
+          }
+        }
       }
     }
     uint32_t grp = head;
