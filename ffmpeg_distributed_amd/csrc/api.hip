@@ -147,7 +147,8 @@ int dmalloc(T **p, size_t count) {
 
 struct PlaneScale {
   SwsFilter hf, vf;
-  int32_t *hcp = nullptr, *hp = nullptr, *vcp = nullptr, *vps = nullptr;
+  int32_t *hcp = nullptr, *hp = nullptr, *vcp = nullptr, *vps = nullptr, *hsum = nullptr;
+  bool d4 = false;  // h coefficients in the v_dot4 hi/lo byte layout (k_scale D4)
   ScaleGeom g{};
   size_t lds = 0;
   dim3 grid;
@@ -227,6 +228,7 @@ void free_ctx(mjg_ctx *c) {
   if (c->tail) (void)hipStreamSynchronize(c->tail);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_stage_bits, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
+                  c->ps[0].hsum, c->ps[1].hsum,
                   c->ps[1].vps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -271,10 +273,30 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   // shifted by its parity and zero-padded to npv = vt/2 + 1 pairs
   const int npv = vt / 2 + 1;
   std::vector<int32_t> hcp((size_t)dw * (ht / 2)), vcp((size_t)dh * npv, 0), vps(dh);
-  for (int x = 0; x < dw; x++)
-    for (int k = 0; k < ht / 2; k++)
-      hcp[(size_t)x * (ht / 2) + k] = (int32_t)((uint32_t)(uint16_t)p.hf.coeff[(size_t)x * ht + 2 * k] |
-                                                ((uint32_t)(uint16_t)p.hf.coeff[(size_t)x * ht + 2 * k + 1] << 16));
+  // D4 layout when every coefficient splits as 128 ch + cl, ch int8, cl in [-64, 64): per 4
+  // taps one word of ch bytes and one of cl bytes (MJG_SCALE_NO_D4=1: the pair layout)
+  std::vector<int32_t> hsum(dw, 0);
+  p.d4 = getenv("MJG_SCALE_NO_D4") == nullptr;
+  for (size_t i = 0; i < p.hf.coeff.size(); i++)
+    if (p.hf.coeff[i] < -128 * 128 - 64 || p.hf.coeff[i] >= 127 * 128 + 64) p.d4 = false;
+  for (int x = 0; x < dw; x++) {
+    const int16_t *cx = &p.hf.coeff[(size_t)x * ht];
+    for (int k = 0; k < ht; k++) hsum[x] += cx[k];
+    for (int k = 0; k < ht / 2; k++) {
+      uint32_t wv;
+      if (p.d4) {
+        const int g4 = k >> 1, lo_part = k & 1;  // word 2j: ch of taps 4j..4j+3, word 2j+1: cl
+        wv = 0;
+        for (int b = 0; b < 4; b++) {
+          const int cv = cx[4 * g4 + b], cl = ((cv + 64) & 127) - 64, ch = (cv - cl) / 128;
+          wv |= (uint32_t)(uint8_t)(int8_t)(lo_part ? cl : ch) << (8 * b);
+        }
+      } else {
+        wv = (uint32_t)(uint16_t)cx[2 * k] | ((uint32_t)(uint16_t)cx[2 * k + 1] << 16);
+      }
+      hcp[(size_t)x * (ht / 2) + k] = (int32_t)wv;
+    }
+  }
   for (int y = 0; y < dh; y++) {
     const int r = p.vf.pos[y], par = r & 1;
     vps[y] = r >> 1;
@@ -300,14 +322,16 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   g.npv = npv;
   g.lds_pairs = max_pairs;
   g.lds_win_words = 2 * max_pairs * max_nw;
-  p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW) * 4;
+  p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW + (size_t)kScaleTileH * (npv + 1)) * 4;
   if (p.lds > 64 * 1024)
     return set_err(MJG_E_INVALID, "scale ratio too large for one LDS tile (%zu B)", p.lds);
   p.grid = dim3((dw + kScaleTileW - 1) / kScaleTileW, (dh + kScaleTileH - 1) / kScaleTileH, 1);
   int rc;
   if ((rc = dmalloc(&p.hcp, hcp.size())) || (rc = dmalloc(&p.hp, (size_t)dw)) ||
-      (rc = dmalloc(&p.vcp, vcp.size())) || (rc = dmalloc(&p.vps, (size_t)dh)))
+      (rc = dmalloc(&p.vcp, vcp.size())) || (rc = dmalloc(&p.vps, (size_t)dh)) ||
+      (rc = dmalloc(&p.hsum, (size_t)dw)))
     return rc;
+  HIP_TRY(hipMemcpy(p.hsum, hsum.data(), (size_t)dw * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(p.hcp, hcp.data(), hcp.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(p.hp, p.hf.pos.data(), (size_t)dw * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(p.vcp, vcp.data(), vcp.size() * 4, hipMemcpyHostToDevice));
@@ -674,12 +698,22 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       }
       dim3 grid = ps.grid;
       grid.z = n;
+#define MJG_SCALE_LAUNCH(HT, NPV)                                                                 \
+  do {                                                                                            \
+    if (ps.d4)                                                                                    \
+      k_scale<HT, NPV, true><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
+                                                               ps.vcp, ps.vps, ps.hsum);          \
+    else                                                                                          \
+      k_scale<HT, NPV, false><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
+                                                                ps.vcp, ps.vps, ps.hsum);         \
+  } while (0)
       if (sg.htaps == 8 && sg.npv == 5)  // 2:1 downscale (4K -> 1080p)
-        k_scale<8, 5><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
+        MJG_SCALE_LAUNCH(8, 5);
       else if (sg.htaps == 4 && sg.npv == 3)  // upscale / mild downscale
-        k_scale<4, 3><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
+        MJG_SCALE_LAUNCH(4, 3);
       else
-        k_scale<0, 0><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, ps.vcp, ps.vps);
+        MJG_SCALE_LAUNCH(0, 0);
+#undef MJG_SCALE_LAUNCH
     }
     tmark(c, S, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());

@@ -12,6 +12,10 @@
 //           column: taps funnel-shifted out of aligned LDS dwords (v_alignbit), widened to
 //           u16 pairs with v_perm and multiplied with v_dot2_i32_i16 against the column's
 //           coefficient pairs (registers).  Rows 2p and 2p+1 go to LDS as one int16 pair.
+//           D4 (every coefficient c = 128 ch + cl with int8 ch, cl in [-64, 64)): the window
+//           is staged level-shifted (byte ^ 0x80 = p - 128 as int8) and four taps are one
+//           v_dot4_i32_i8 against the hi and one against the lo bytes, no widening:
+//           sum p c >> 7 = ah + (al >> 7) + sum c (exact: 128 (ah + sum c) is a multiple of 128).
 //   v-pass: output row y reads the pairs [vps[y], vps[y] + npv) of its column and dot2s
 //           them against that row's coefficient pairs, which the host pre-shifts by the
 //           parity of the first tap row (zero-padded), so odd and even starts cost the same.
@@ -40,26 +44,38 @@ struct ScaleGeom {
 };
 
 __device__ __forceinline__ int sws_range(int v, int range) {
-  if (range == 1) {
+  if (range == 1) {  // |v| < 2^15: the 24-bit multiply is exact
     v = min(v, 30189);
-    return (v * 19077 - 39057361) >> 14;
+    return (__mul24(v, 19077) - 39057361) >> 14;
   }
   if (range == 2) {
     v = min(v, 30775);
-    return (v * 4663 - 9289992) >> 12;
+    return (__mul24(v, 4663) - 9289992) >> 12;
   }
   return v;
 }
 
 // hScale8To15 of one source row (taps = the `htaps` bytes at byte offset `off` of an LDS
 // row), then range conversion.  Bytes are fetched as aligned dwords and funnel-shifted.
-template <int HT>  // 0: runtime htaps
+template <int HT, bool D4>  // HT 0: runtime htaps
 __device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const int32_t *hcp, int htaps_rt,
-                                          int range) {
+                                          int range, int hs) {
   const int htaps = HT ? HT : htaps_rt;
   const uint32_t *q = row + (off >> 2);
   const uint32_t sh = (uint32_t)(off & 3) * 8;
   uint32_t lo = q[0];
+  if (D4) {
+    int ah = 0, al = 0;
+#pragma unroll
+    for (int k = 0; k < htaps; k += 4) {
+      const uint32_t hi = q[(k >> 2) + 1];
+      const int w = (int)__builtin_amdgcn_alignbit(hi, lo, sh);  // taps k..k+3, int8 p - 128
+      lo = hi;
+      ah = __builtin_amdgcn_sdot4(w, hcp[k >> 1], ah, false);
+      al = __builtin_amdgcn_sdot4(w, hcp[(k >> 1) + 1], al, false);
+    }
+    return sws_range(min(ah + (al >> 7) + hs, 32767), range);
+  }
   int acc = 0;
 #pragma unroll
   for (int k = 0; k < htaps; k += 4) {
@@ -77,83 +93,106 @@ __device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const in
 typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 
 // HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio)
-template <int HT, int NPV>
+template <int HT, int NPV, bool D4>
 __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
                                                uint8_t *__restrict__ dst, ScaleGeom g,
                                                const int32_t *__restrict__ hcp,   // [dw][htaps/2]
                                                const int32_t *__restrict__ hp,    // [dw]
                                                const int32_t *__restrict__ vcp,   // [dh][npv]
-                                               const int32_t *__restrict__ vps) { // [dh] pair start
+                                               const int32_t *__restrict__ vps,   // [dh] pair start
+                                               const int32_t *__restrict__ hsum) {  // D4: [dw] sum of taps
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a uniform value: the v-pass rows (and their filter rows) are wave-uniform
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * kScaleTileH, f = blockIdx.z;
   const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off;
   uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off;
   const int xe = min(x0 + kScaleTileW, g.dw), ye = min(y0 + kScaleTileH, g.dh);
   const int p0 = vps[y0], p1 = vps[ye - 1] + g.npv;  // row pairs [p0, p1)
   const int nrows = 2 * (p1 - p0);
+  const int npv = NPV ? NPV : g.npv;
   // source window: dwords [cb, cb + nw) of rows [2 p0, 2 p1) (rows clamped to the plane;
   // the rows past it only meet zero coefficients), staged with coalesced dword loads
   const int cb = hp[x0] & ~3;
   const int nw = ((hp[xe - 1] + g.htaps - cb + 3) >> 2) + 1;  // +1: the funnel shift reads one past
   uint32_t *win = smem;                                       // [nrows][nw]
   uint32_t *pairs = smem + g.lds_win_words;                   // [p1 - p0][64]
-  if (nw <= 64 && nrows <= 4 * kScaleMaxRowsPerWave && g.sw >= 4) {
-    // wave per row, lane per dword; all of a wave's loads issued before any is waited on.
-    // A dword crossing the row end is loaded from sw-4 and shifted down (bytes >= sw are
-    // never used).
-    uint32_t v[kScaleMaxRowsPerWave];
-    const int col = cb + 4 * lane, lcol = min(col, g.sw - 4);
-    const uint32_t drop = (uint32_t)(col - lcol) * 8;
+  uint32_t *vtab = pairs + g.lds_pairs * kScaleTileW;         // [ye - y0][1 + npv]: pair start, coefficients
+  const bool fast = nw <= 64 && nrows <= 4 * kScaleMaxRowsPerWave && g.sw >= 4;
+  // Every global load of the tile is issued before any is waited on: the window rows, this
+  // lane's h filter (column x), and the tile's v filter rows (one entry per thread).
+  uint32_t v[kScaleMaxRowsPerWave];
+  const int col = cb + 4 * lane, lcol = min(col, max(g.sw - 4, 0));
+  const uint32_t drop = (uint32_t)(col - lcol) * 8;
+  if (fast) {
+    // wave per row, lane per dword.  A dword crossing the row end is loaded from sw-4 and
+    // shifted down (bytes >= sw are never used).
     const uint8_t *sc = s + lcol;
 #pragma unroll
     for (int j = 0; j < kScaleMaxRowsPerWave; j++)  // unconditional: every address is in-plane
       v[j] = *(const u32_unaligned *)(sc + (size_t)min(2 * p0 + wave + 4 * j, g.sh - 1) * g.s_stride);
-#pragma unroll
-    for (int j = 0; j < kScaleMaxRowsPerWave; j++) {
-      const int r = wave + 4 * j;
-      if (r < nrows && lane < nw) win[r * nw + lane] = v[j] >> drop;
-    }
-  } else {
-    for (int i = tid; i < nrows * nw; i += 256) {
-      const int r = i / nw, c = i - r * nw;
-      const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
-      const int col = cb + 4 * c;
-      uint32_t v = 0;
-      for (int bb = 0; bb < 4; bb++)
-        if (col + bb < g.sw) v |= (uint32_t)rp[col + bb] << (8 * bb);
-      win[i] = v;
-    }
   }
   const int x = min(x0 + lane, g.dw - 1);  // clamped: tail lanes redo the last column
   const int32_t *hc = hcp + (size_t)x * (g.htaps >> 1);
   int32_t hreg[HT ? HT / 2 : 8];  // HT taps (or up to 16 at runtime) in registers
 #pragma unroll
   for (int k = 0; k < (HT ? HT / 2 : 8); k++) hreg[k] = (2 * k < g.htaps) ? hc[k] : 0;
-  const int off = hp[x] - cb;
+  const int hpx = hp[x];
+  const int hs = D4 ? hsum[x] : 0;
+  const int nvt = (ye - y0) * (npv + 1);
+  uint32_t vt = 0;
+  int vi = tid;
+  if (vi < nvt) {
+    const int yy = vi / (npv + 1), k = vi - yy * (npv + 1);
+    vt = k == 0 ? (uint32_t)vps[y0 + yy] : (uint32_t)vcp[(size_t)(y0 + yy) * g.npv + (k - 1)];
+  }
+  if (fast) {
+#pragma unroll
+    for (int j = 0; j < kScaleMaxRowsPerWave; j++) {
+      const int r = wave + 4 * j;
+      if (r < nrows && lane < nw) win[r * nw + lane] = (v[j] >> drop) ^ (D4 ? 0x80808080u : 0u);
+    }
+  } else {
+    for (int i = tid; i < nrows * nw; i += 256) {
+      const int r = i / nw, c = i - r * nw;
+      const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
+      const int cc = cb + 4 * c;
+      uint32_t w = 0;
+      for (int bb = 0; bb < 4; bb++)
+        if (cc + bb < g.sw) w |= (uint32_t)rp[cc + bb] << (8 * bb);
+      win[i] = w ^ (D4 ? 0x80808080u : 0u);
+    }
+  }
+  for (; vi < nvt; vi += 256) {  // (one pass unless npv > 7)
+    if (vi != tid) {
+      const int yy = vi / (npv + 1), k = vi - yy * (npv + 1);
+      vt = k == 0 ? (uint32_t)vps[y0 + yy] : (uint32_t)vcp[(size_t)(y0 + yy) * g.npv + (k - 1)];
+    }
+    vtab[vi] = vt;
+  }
+  const int off = hpx - cb;
   __syncthreads();
   for (int p = wave; p < p1 - p0; p += 4) {
     int a, b;
     if (HT || g.htaps <= 16) {
-      a = hscale_lds<HT>(win + (2 * p) * nw, off, hreg, g.htaps, g.range);
-      b = hscale_lds<HT>(win + (2 * p + 1) * nw, off, hreg, g.htaps, g.range);
+      a = hscale_lds<HT, D4>(win + (2 * p) * nw, off, hreg, g.htaps, g.range, hs);
+      b = hscale_lds<HT, D4>(win + (2 * p + 1) * nw, off, hreg, g.htaps, g.range, hs);
     } else {
-      a = hscale_lds<0>(win + (2 * p) * nw, off, hc, g.htaps, g.range);
-      b = hscale_lds<0>(win + (2 * p + 1) * nw, off, hc, g.htaps, g.range);
+      a = hscale_lds<0, D4>(win + (2 * p) * nw, off, hc, g.htaps, g.range, hs);
+      b = hscale_lds<0, D4>(win + (2 * p + 1) * nw, off, hc, g.htaps, g.range, hs);
     }
     pairs[p * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
   }
   __syncthreads();
   if (x0 + lane >= g.dw) return;
   for (int y = y0 + wave; y < ye; y += 4) {
-    const int32_t *vc = vcp + (size_t)y * g.npv;
-    const uint32_t *col = pairs + (vps[y] - p0) * 64 + lane;
+    const uint32_t *vr = vtab + (y - y0) * (npv + 1);  // uniform address: LDS broadcast
+    const uint32_t *cp = pairs + ((int)vr[0] - p0) * 64 + lane;
     int acc = 64 << 12;
-    const int npv = NPV ? NPV : g.npv;
 #pragma unroll
     for (int k = 0; k < npv; k++)
-      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, col[k * 64]),
-                                   __builtin_bit_cast(short2_t, vc[k]), acc, false);
+      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, cp[k * 64]),
+                                   __builtin_bit_cast(short2_t, vr[1 + k]), acc, false);
     d[(size_t)y * g.d_stride + x0 + lane] = (uint8_t)min(max(acc >> 19, 0), 255);
   }
 }

@@ -15,6 +15,8 @@ def main():
     p.add_argument("--w", type=int, default=3840)
     p.add_argument("--h", type=int, default=2160)
     p.add_argument("--q", type=int, default=5)
+    p.add_argument("--dw", type=int, default=None, help="scaled width (-vf scale)")
+    p.add_argument("--dh", type=int, default=None)
     a = p.parse_args()
     import torch
     from ffmpeg_distributed_amd.encoder import MjpegEncoder
@@ -26,7 +28,7 @@ def main():
         k = min(20, a.frames - i)
         pool[i:i + k] = testsrc2_i420_torch(a.w, a.h, i, k, dev)
     torch.cuda.synchronize()
-    enc = MjpegEncoder(0, a.w, a.h, qscale=a.q, max_batch=a.frames)
+    enc = MjpegEncoder(0, a.w, a.h, dst_w=a.dw, dst_h=a.dh, qscale=a.q, max_batch=a.frames)
     tot = 0
     for _ in range(a.launches):
         enc.submit(device_ptr=pool.data_ptr(), nframes=a.frames)
