@@ -698,14 +698,24 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       }
       dim3 grid = ps.grid;
       grid.z = n;
-#define MJG_SCALE_LAUNCH(HT, NPV)                                                                 \
+#define MJG_SCALE_LAUNCH3(HT, NPV, D4)                                                            \
   do {                                                                                            \
-    if (ps.d4)                                                                                    \
-      k_scale<HT, NPV, true><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
-                                                               ps.vcp, ps.vps, ps.hsum);          \
-    else                                                                                          \
-      k_scale<HT, NPV, false><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
+    if (sg.range == 1)                                                                            \
+      k_scale<HT, NPV, D4, 1><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
                                                                 ps.vcp, ps.vps, ps.hsum);         \
+    else if (sg.range == 2)                                                                       \
+      k_scale<HT, NPV, D4, 2><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
+                                                                ps.vcp, ps.vps, ps.hsum);         \
+    else                                                                                          \
+      k_scale<HT, NPV, D4, 0><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
+                                                                ps.vcp, ps.vps, ps.hsum);         \
+  } while (0)
+#define MJG_SCALE_LAUNCH(HT, NPV)      \
+  do {                                 \
+    if (ps.d4)                         \
+      MJG_SCALE_LAUNCH3(HT, NPV, true);  \
+    else                               \
+      MJG_SCALE_LAUNCH3(HT, NPV, false); \
   } while (0)
       if (sg.htaps == 8 && sg.npv == 5)  // 2:1 downscale (4K -> 1080p)
         MJG_SCALE_LAUNCH(8, 5);
@@ -714,6 +724,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       else
         MJG_SCALE_LAUNCH(0, 0);
 #undef MJG_SCALE_LAUNCH
+#undef MJG_SCALE_LAUNCH3
     }
     tmark(c, S, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());

@@ -93,7 +93,7 @@ __device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const in
 typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 
 // HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio)
-template <int HT, int NPV, bool D4>
+template <int HT, int NPV, bool D4, int RANGE>  // RANGE: g.range as a compile-time value
 __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
                                                uint8_t *__restrict__ dst, ScaleGeom g,
                                                const int32_t *__restrict__ hcp,   // [dw][htaps/2]
@@ -172,14 +172,15 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   }
   const int off = hpx - cb;
   __syncthreads();
+#pragma unroll 2
   for (int p = wave; p < p1 - p0; p += 4) {
     int a, b;
     if (HT || g.htaps <= 16) {
-      a = hscale_lds<HT, D4>(win + (2 * p) * nw, off, hreg, g.htaps, g.range, hs);
-      b = hscale_lds<HT, D4>(win + (2 * p + 1) * nw, off, hreg, g.htaps, g.range, hs);
+      a = hscale_lds<HT, D4>(win + (2 * p) * nw, off, hreg, g.htaps, RANGE, hs);
+      b = hscale_lds<HT, D4>(win + (2 * p + 1) * nw, off, hreg, g.htaps, RANGE, hs);
     } else {
-      a = hscale_lds<0, D4>(win + (2 * p) * nw, off, hc, g.htaps, g.range, hs);
-      b = hscale_lds<0, D4>(win + (2 * p + 1) * nw, off, hc, g.htaps, g.range, hs);
+      a = hscale_lds<0, D4>(win + (2 * p) * nw, off, hc, g.htaps, RANGE, hs);
+      b = hscale_lds<0, D4>(win + (2 * p + 1) * nw, off, hc, g.htaps, RANGE, hs);
     }
     pairs[p * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
   }
