@@ -1320,7 +1320,7 @@ __device__ __forceinline__ GroupWords group_words(const uint32_t *scratch, const
 // issue the loads of several words before using any: word_load finds the owner chunk c
 // (relative to the group; uniform readlane compares) and loads the three slot words the
 // word can need (independent, unconditional loads), word_value assembles it.  Bits past the
-// chunk come from chunk c+1's first word, or for the segment's last chunk are the 1-bit
+// chunk come from chunk c+1's first word; past the segment's last bit comes the 1-bit
 // padding to a byte boundary (ff_mjpeg_escape_FF pad).  k must lie in [k0, k1).
 struct WordLoad {
   uint32_t w0, w1, w2, L, NL, p;
@@ -1348,17 +1348,21 @@ __device__ __forceinline__ WordLoad word_load(const GroupWords &g, uint32_t k) {
   return r;
 }
 
-__device__ __forceinline__ uint32_t word_value(const GroupWords &g, const WordLoad &r) {
+__device__ __forceinline__ uint32_t word_value(const GroupWords &g, const WordLoad &r, uint32_t k) {
   const uint32_t wi = r.p >> 5, s = r.p & 31, nw = (r.L + 31) >> 5;
   const uint32_t w1 = wi + 1 < nw ? r.w1 : 0u;
   uint32_t v = s ? (r.w0 << s) | (w1 >> (32 - s)) : r.w0;
   const uint32_t rem = r.L - r.p;  // > 0: the word's first bit lies in its chunk
   if (rem < 32) {
     v &= ~(0xffffffffu >> rem);
-    const uint32_t nv = r.NL < 32 ? r.w2 & ~(0xffffffffu >> r.NL) : r.w2;
+    if (r.has_next) v |= (r.NL < 32 ? r.w2 & ~(0xffffffffu >> r.NL) : r.w2) >> rem;
+  }
+  // The segment ends in this word: 1-bit padding to the byte boundary.  The word's owner
+  // need not be the last chunk: a short last chunk can start and end inside it.
+  const uint32_t endk = g.T - 32 * k;  // >= 1 (word k < k1)
+  if (endk < 32) {
     const uint32_t pad = (8 - (g.T & 7)) & 7;
-    const uint32_t ones = (0xffffffffu >> rem) & ~(rem + pad >= 32 ? 0u : (0xffffffffu >> (rem + pad)));
-    v |= r.has_next ? nv >> rem : ones;
+    v |= (0xffffffffu >> endk) & ~(endk + pad >= 32 ? 0u : (0xffffffffu >> (endk + pad)));
   }
   return v;
 }
@@ -1388,7 +1392,7 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
     for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
     uint32_t v[kWordsPerLane];
 #pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i]);
+    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
 #pragma unroll
     for (int i = 0; i < kWordsPerLane; i++) {
       const uint32_t k = kb + 64 * i + lane;
@@ -1549,7 +1553,7 @@ __global__ __launch_bounds__(256) void k_write(
     for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
     uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
 #pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i]);
+    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
 #pragma unroll
     for (int i = 0; i < kWordsPerLane; i++) {
       const uint32_t k = kb + 64 * i + lane;

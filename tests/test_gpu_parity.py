@@ -44,6 +44,16 @@ def rand_frames(w, h, n, seed, kind="noise", chroma="420"):
             v = (255 - u).astype(np.uint8)
             out.append(pack_i420(y, u, v))
         return np.stack(out)
+    if kind == "patches":  # flat picture with noisy 8x8 patches: a few long blocks per chunk
+        out = []
+        for i in range(n):
+            f = np.full(fb, 96, np.uint8)
+            y = f[: w * h].reshape(h, w)
+            for _ in range(max(1, (w // 8) * (h // 8) // 12)):
+                by, bx = rng.integers(0, max(1, h // 8)), rng.integers(0, max(1, w // 8))
+                y[by * 8:by * 8 + 8, bx * 8:bx * 8 + 8] = rng.integers(0, 256, (8, 8))[: h - by * 8, : w - bx * 8]
+            out.append(f)
+        return np.stack(out)
     if kind == "testsrc":
         out = []
         for i in range(n):
@@ -87,6 +97,13 @@ CASES = [
     (101, 57, 7, True, "smooth"),
     (1920, 1080, 5, False, "testsrc"),
     (1280, 720, 2, True, "noise"),
+    # blocks past 128 bits staged in HBM among short ones (k_encode ShiftSink spill/flush)
+    (256, 128, 1, True, "patches"),
+    (200, 72, 2, False, "patches"),
+    # a short last chunk (2 / 6 blocks) that starts and ends inside the frame's last word:
+    # the byte padding must still be applied (the word's owner is the chunk before it)
+    (176, 16, 5, True, "flat"),
+    (176, 16, 5, False, "patches"),
 ]
 
 
