@@ -175,6 +175,7 @@ struct Slot {
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
   uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;  // optimal
+  uint32_t *d_syms = nullptr, *d_symn = nullptr;  // optimal: per block, the symbols the counting pass saw
   uint8_t *d_dht = nullptr;
   int16_t *d_dbg = nullptr;
   uint64_t *h_sizes = nullptr;
@@ -204,6 +205,7 @@ struct mjg_ctx {
   uint32_t *d_stage_bits = nullptr;  // k_encode: per wave, lane-major staging of blocks past 128 bits
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
+  bool reencode = false;       // optimal: emission pass recomputes the blocks (MJG_OPT_REENCODE=1)
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
@@ -235,7 +237,7 @@ void free_ctx(mjg_ctx *c) {
   for (Slot &S : c->slot) {
     void *sp[] = {S.d_scratch, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
                   S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_out,
-                  S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg};
+                  S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg, S.d_syms, S.d_symn};
     for (void *p : sp)
       if (p) (void)hipFree(p);
     if (S.h_sizes) (void)hipHostFree(S.h_sizes);
@@ -358,7 +360,8 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   if (c->optimal &&
       ((rc = dmalloc(&S.d_hist, B * kFrameTabWords)) || (rc = dmalloc(&S.d_ftabs, B * kFrameTabWords)) ||
        (rc = dmalloc(&S.d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&S.d_dht_nval, B * 4)) ||
-       (rc = dmalloc(&S.d_hdr_lens, B))))
+       (rc = dmalloc(&S.d_hdr_lens, B)) || (rc = dmalloc(&S.d_syms, B * NC * (size_t)kSymCap * 64)) ||
+       (rc = dmalloc(&S.d_symn, B * NC * 64))))
     return rc;
   if (g.debug_coefs && (rc = dmalloc(&S.d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
 #ifdef MJG_STAMPS
@@ -445,6 +448,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
                         c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
+  c->reencode = getenv("MJG_OPT_REENCODE") != nullptr;
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
@@ -611,11 +615,11 @@ void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntas
   if (g.range_convert)
     k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        S.d_ftabs, c->d_stage_bits);
+        S.d_ftabs, c->d_stage_bits, S.d_syms, S.d_symn);
   else
     k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        S.d_ftabs, c->d_stage_bits);
+        S.d_ftabs, c->d_stage_bits, S.d_syms, S.d_symn);
 }
 
 }  // namespace
@@ -743,8 +747,12 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     HIP_TRY(hipGetLastError());
   }
   tmark(c, S, MJG_K_ENCODE, 0);
-  if (c->optimal)
+  if (c->optimal && c->reencode)  // MJG_OPT_REENCODE=1: recompute the blocks (A/B)
     launch_encode<kEmitFrame>(c, S, enc_in, wgs, ntasks);
+  else if (c->optimal)
+    k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, c->stream>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
+                                                                  S.d_scratch, S.d_chunk_bits, c->d_stage_bits,
+                                                                  ntasks);
   else
     launch_encode<kEmitDefault>(c, S, enc_in, wgs, ntasks);
   tmark(c, S, MJG_K_ENCODE, 1);

@@ -333,10 +333,24 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
 // -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
 // (layout of the table block: AC luma 0-255, AC chroma 256-511, DC luma 512-527,
 // DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.
+// It also records every symbol with its mantissa in the lane's record column (rec[j * 64]:
+// DC flag << 31 | (DC category or AC symbol) << 16 | mantissa), so the emission pass
+// replays the symbols (k_emit_syms) instead of recomputing the block.
+constexpr int kSymCap = 68;  // symbols per block: DC + 63 AC + 3 ZRL + EOB
 struct CountSink {
   uint32_t *hac, *hdc;
-  __device__ __forceinline__ void dc(int cat, uint32_t) { atomicAdd(&hdc[cat], 1u); }
-  __device__ __forceinline__ void ac(int sym, int, uint32_t) { atomicAdd(&hac[sym], 1u); }
+  uint32_t *rec;
+  uint32_t n = 0;
+  __device__ __forceinline__ void dc(int cat, uint32_t mant) {
+    atomicAdd(&hdc[cat], 1u);
+    rec[n * 64] = (1u << 31) | ((uint32_t)cat << 16) | mant;
+    n++;
+  }
+  __device__ __forceinline__ void ac(int sym, int, uint32_t mant) {
+    atomicAdd(&hac[sym], 1u);
+    rec[n * 64] = ((uint32_t)sym << 16) | mant;
+    n++;
+  }
   __device__ __forceinline__ void finish() {}
 };
 
@@ -475,12 +489,80 @@ __device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, boo
 constexpr int kEmitDefault = 0, kCount = 1, kEmitFrame = 2;
 constexpr int kFrameTabWords = 544;  // AC luma, AC chroma, DC luma, DC chroma (table block layout)
 
+// Pack a chunk's 64 block codes into its slot: a wave prefix-scan of the block lengths gives
+// each block's bit offset; blocks up to 128 bits come from their ShiftSink window, longer
+// ones from their staging column.  No LDS atomics: lane L's bits occupy words fw..lw.
+// Words strictly inside are L's alone; word fw may be shared with earlier lanes and word lw
+// with later ones.  Every word has one writer: the lane whose bits cover its first bit
+// ("opener"), which ORs in the heads of the lanes that start inside the word, G = segmented
+// suffix-OR of heads over lanes with equal fw.  Lane 0 writes the chunk's bit count.
+__device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, uint32_t *slot,
+                                           uint32_t *chunk_bits_t, int lane) {
+  const uint32_t incl = wave_incl_scan(q.bits, lane);
+  const uint32_t off = incl - q.bits;
+  const uint32_t total = __shfl(incl, 63, 64);
+
+  const bool has = cur_active && q.bits != 0;
+  const uint32_t sft = off & 31, fw = off >> 5;
+  const uint32_t lw = has ? (off + q.bits - 1) >> 5 : fw;
+  uint32_t head = 0, tail = 0;
+  if (has && MJG_ABLATE != 4) {
+    if (q.bits <= 128 || MJG_ABLATE == 7) {
+      // the block's words from its end: d[4] = word lw, d[4 - j] = word lw - j, i.e. the
+      // right-aligned 128 bits shifted left by t, the free bits after the block in word lw
+      const uint32_t t = (32u - ((off + q.bits) & 31u)) & 31u, sh = 32u - t;  // sh in 1..32
+      const uint32_t d[5] = {(uint32_t)((uint64_t)q.w0 >> sh),
+                             (uint32_t)((((uint64_t)q.w0 << 32) | q.w1) >> sh),
+                             (uint32_t)((((uint64_t)q.w1 << 32) | q.w2) >> sh),
+                             (uint32_t)((((uint64_t)q.w2 << 32) | q.w3) >> sh), q.w3 << t};
+      const uint32_t nmid = lw - fw;  // 0..4
+      tail = d[4];
+#pragma unroll
+      for (int j = 1; j < 4; j++)
+        if ((uint32_t)j < nmid) slot[lw - j] = d[4 - j];
+      head = nmid == 0 ? d[4] : nmid == 1 ? d[3] : nmid == 2 ? d[2] : nmid == 3 ? d[1] : d[0];
+    } else {  // long block: its staged stream shifted into place, 8 words per step
+      const uint32_t nws = (q.bits + 31) >> 5, nw = lw - fw + 1;
+      const uint32_t *stg = q.stage;
+      for (uint32_t m0 = 0; m0 < nw; m0 += 8) {
+        uint32_t S[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {  // stream words m0 - 1 .. m0 + 7 (0 outside the stream)
+          const uint32_t j = m0 - 1 + (uint32_t)i;
+          S[i] = j < nws ? stg[j * 64] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const uint32_t m = m0 + (uint32_t)i;
+          const uint32_t F = sft ? (S[i] << (32u - sft)) | (S[i + 1] >> sft) : S[i + 1];
+          if (m == 0) head = F;
+          if (m + 1 == nw && m > 0) tail = F;
+          if (m > 0 && m + 1 < nw) slot[fw + m] = F;
+        }
+      }
+    }
+  }
+  uint32_t grp = head;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_down(grp, d, 64), f = __shfl_down(fw, d, 64);
+    if (lane + d < 64 && f == fw) grp |= v;
+  }
+  const uint32_t gnext = __shfl_down(grp, 1, 64), fnext = __shfl_down(fw, 1, 64);
+  if (has && MJG_ABLATE != 4) {
+    if (lw > fw) slot[lw] = tail | ((lane < 63 && fnext == lw) ? gnext : 0u);
+    if (sft == 0) slot[fw] = grp;  // word-aligned start: this lane opens word fw
+  }
+  if (lane == 0) *chunk_bits_t = total;
+}
+
 template <bool RC, int MODE>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
-    uint32_t *__restrict__ hist, const uint32_t *__restrict__ ftabs, uint32_t *__restrict__ stage_all) {
+    uint32_t *__restrict__ hist, const uint32_t *__restrict__ ftabs, uint32_t *__restrict__ stage_all,
+    uint32_t *__restrict__ syms, uint32_t *__restrict__ symn) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
@@ -862,10 +944,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       aux_frame = cur_frame;
     }
     if (MODE == kCount) {
-      if (cur_active) {
-        CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16};
-        emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
-      }
+      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kSymCap * 64 + lane};
+      if (cur_active) emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
+      symn[(size_t)t * 64 + lane] = cs.n;
       if (tn < 0) break;
       if (new_batch) {
         carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
@@ -892,68 +973,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       q.finish();
     }
 #endif
-    const uint32_t incl = wave_incl_scan(q.bits, lane);
-    const uint32_t off = incl - q.bits;
-    const uint32_t total = __shfl(incl, 63, 64);
-    uint32_t *slot = scratch + (size_t)t * kSlotWords;
-
-    // Pack into the chunk slot without LDS atomics.  Lane L's bits occupy words fw..lw.
-    // Words strictly inside are L's alone; word fw may be shared with earlier lanes and
-    // word lw with later ones.  Every word has one writer: the lane whose bits cover its
-    // first bit ("opener"), which ORs in the heads of the lanes that start inside the
-    // word, G = segmented suffix-OR of heads over lanes with equal fw.
-    const bool has = cur_active && q.bits != 0;
-    const uint32_t sft = off & 31, fw = off >> 5;
-    const uint32_t lw = has ? (off + q.bits - 1) >> 5 : fw;
-    uint32_t head = 0, tail = 0;
-    if (has && MJG_ABLATE != 4) {
-      if (q.bits <= 128 || MJG_ABLATE == 7) {
-        // the block's words from its end: d[4] = word lw, d[4 - j] = word lw - j, i.e. the
-        // right-aligned 128 bits shifted left by t, the free bits after the block in word lw
-        const uint32_t t = (32u - ((off + q.bits) & 31u)) & 31u, sh = 32u - t;  // sh in 1..32
-        const uint32_t d[5] = {(uint32_t)((uint64_t)q.w0 >> sh),
-                               (uint32_t)((((uint64_t)q.w0 << 32) | q.w1) >> sh),
-                               (uint32_t)((((uint64_t)q.w1 << 32) | q.w2) >> sh),
-                               (uint32_t)((((uint64_t)q.w2 << 32) | q.w3) >> sh), q.w3 << t};
-        const uint32_t nmid = lw - fw;  // 0..4
-        tail = d[4];
-#pragma unroll
-        for (int j = 1; j < 4; j++)
-          if ((uint32_t)j < nmid) slot[lw - j] = d[4 - j];
-        head = nmid == 0 ? d[4] : nmid == 1 ? d[3] : nmid == 2 ? d[2] : nmid == 3 ? d[1] : d[0];
-      } else {  // long block: its staged stream shifted into place, 8 words per step
-        const uint32_t nws = (q.bits + 31) >> 5, nw = lw - fw + 1;
-        const uint32_t *stg = q.stage;
-        for (uint32_t m0 = 0; m0 < nw; m0 += 8) {
-          uint32_t S[9];
-#pragma unroll
-          for (int i = 0; i < 9; i++) {  // stream words m0 - 1 .. m0 + 7 (0 outside the stream)
-            const uint32_t j = m0 - 1 + (uint32_t)i;
-            S[i] = j < nws ? stg[j * 64] : 0u;
-          }
-#pragma unroll
-          for (int i = 0; i < 8; i++) {
-            const uint32_t m = m0 + (uint32_t)i;
-            const uint32_t F = sft ? (S[i] << (32u - sft)) | (S[i + 1] >> sft) : S[i + 1];
-            if (m == 0) head = F;
-            if (m + 1 == nw && m > 0) tail = F;
-            if (m > 0 && m + 1 < nw) slot[fw + m] = F;
-          }
-        }
-      }
-    }
-    uint32_t grp = head;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t v = __shfl_down(grp, d, 64), f = __shfl_down(fw, d, 64);
-      if (lane + d < 64 && f == fw) grp |= v;
-    }
-    const uint32_t gnext = __shfl_down(grp, 1, 64), fnext = __shfl_down(fw, 1, 64);
-    if (has && MJG_ABLATE != 4) {
-      if (lw > fw) slot[lw] = tail | ((lane < 63 && fnext == lw) ? gnext : 0u);
-      if (sft == 0) slot[fw] = grp;  // word-aligned start: this lane opens word fw
-    }
-    if (lane == 0) chunk_bits[t] = total;
+    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     if (tn < 0) break;
     if (new_batch) {
       carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
@@ -968,6 +988,60 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       const uint32_t v = s_aux[i];
       if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
     }
+  }
+}
+
+// ------------------------------------------------------------ k_emit_syms
+// -huffman optimal, emission pass: every block's symbols as the counting pass recorded
+// them (CountSink), coded with the frame's tables (k_huff_build) and packed as k_encode
+// packs them.  No pixels, no DCT: one wave per chunk, lane = block; the record words are
+// loaded 4 per step.  Persistent waves (the long-block staging columns are per wave).
+__global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
+    EncGeom g, const uint32_t *__restrict__ tabs, const uint32_t *__restrict__ ftabs,
+    const uint32_t *__restrict__ syms, const uint32_t *__restrict__ symn, uint32_t *__restrict__ scratch,
+    uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ stage_all, int ntasks) {
+  __shared__ uint32_t s_aux_all[kWavesPerWg][kFrameTabWords];
+  __shared__ uint32_t s_desc[8];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < 8) s_desc[tid] = tabs[672 + tid];
+  __syncthreads();
+  uint32_t *s_aux = s_aux_all[wave];
+  const int nwaves = gridDim.x * kWavesPerWg, gw = blockIdx.x * kWavesPerWg + wave;
+  int aux_frame = -1;
+  for (int t = gw; t < ntasks; t += nwaves) {
+    int frame, chunk, bbase;
+    task_pos(g, t, frame, chunk, bbase);
+    if (frame != aux_frame) {  // the frame's code tables into the wave's LDS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = ftabs[(size_t)frame * kFrameTabWords + i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      aux_frame = frame;
+    }
+    const int b = chunk * 64 + lane;
+    const bool active = b < g.seg_blocks;
+    const int tab = desc_tab(s_desc[block_in_mcu(g, b)]);
+    ShiftSink q;
+    q.act = s_aux + tab * 256;
+    q.dct = s_aux + 512 + tab * 16;
+    q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
+    const uint32_t n = active ? symn[(size_t)t * 64 + lane] : 0u;
+    const uint32_t *rec = syms + (size_t)t * kSymCap * 64 + lane;
+    for (uint32_t j0 = 0; j0 < n; j0 += 4) {
+      uint32_t e[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) e[i] = j0 + i < n ? rec[(j0 + i) * 64] : 0u;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (j0 + i >= n) break;
+        const uint32_t v = (e[i] >> 16) & 0xffu, mant = e[i] & 0xffffu;
+        if (e[i] >> 31)
+          q.dc((int)v, mant);
+        else
+          q.ac((int)v, (int)(v & 15u), mant);
+      }
+    }
+    if (q.bits > 128) q.flush();
+    pack_chunk(q, active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
   }
 }
 
