@@ -109,8 +109,11 @@ class FFMPEGProc:
             elif self.update_callback:
                 frame, fps, t, speed = prog
                 self.update_callback(frame, fps, t, self.duration, speed)
+        # stderr can reach EOF a moment before the child exits: the reference's loop runs
+        # until poll() sees the exit (fd.py:62), so wait for it unless stop() was called
+        # (then, like fd.py:85-89, give it one second and report whatever is there)
         try:
-            rest = self.proc.communicate(timeout=1)[1]
+            rest = self.proc.communicate(timeout=None if not self._stop.is_set() else 1)[1]
             self.stderr += rest or ""
         except subprocess.TimeoutExpired:
             pass

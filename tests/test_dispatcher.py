@@ -62,7 +62,9 @@ def norm_md5(text):
 
 def canon_calls(calls):
     """Split and concat calls in order; worker calls as a multiset (host assignment is
-    dynamic pull, so which host ran which segment is not deterministic)."""
+    dynamic pull, so which host ran which segment is not deterministic); ssh hops as the
+    set of distinct remote commands (how many segments went through ssh varies per run,
+    in the reference as here)."""
     def role(c):
         a = c.get("argv", [])
         if c["prog"] == "ssh":
@@ -74,8 +76,9 @@ def canon_calls(calls):
         return "worker"
     seq = [c for c in calls if role(c) in ("split", "concat")]
     workers = sorted(json.dumps({k: v for k, v in c.items() if k != "host"}, sort_keys=True)
-                     for c in calls if role(c) in ("worker", "ssh"))
-    return seq, workers
+                     for c in calls if role(c) == "worker")
+    ssh = sorted({c["cmd"] for c in calls if role(c) == "ssh"})
+    return seq, workers, ssh
 
 
 @pytest.mark.parametrize("name", sorted(FX["scenarios"]))
