@@ -176,13 +176,22 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
+// Inclusive wave prefix sum on DPP lane moves (no LDS round trips): Hillis-Steele within
+// each 16-lane row (row_shr 1, 2, 4, 8; lanes whose source is outside the row add the
+// `old` 0), then row_bcast:15 carries row 0 / row 2 totals into rows 1 / 3 and
+// row_bcast:31 carries the rows 0-1 total into rows 2-3.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
+}
+
+__device__ __forceinline__ uint32_t lane63(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -500,7 +509,7 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
                                            uint32_t *chunk_bits_t, int lane) {
   const uint32_t incl = wave_incl_scan(q.bits, lane);
   const uint32_t off = incl - q.bits;
-  const uint32_t total = __shfl(incl, 63, 64);
+  const uint32_t total = lane63(incl);
 
   const bool has = cur_active && q.bits != 0;
   const uint32_t sft = off & 31, fw = off >> 5;
@@ -542,13 +551,18 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
       }
     }
   }
+  // Every active block is at least 2 bits (a DC code and an EOB or coefficient-63 code,
+  // each >= 1 bit), so at most 16 active lanes start inside one word: distances 1..15
+  // (steps 1, 2, 4, 8) reach the whole group.  Inactive lanes (the chunk's tail) add 0.
   uint32_t grp = head;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
+  for (int d = 1; d < 16; d <<= 1) {
     const uint32_t v = __shfl_down(grp, d, 64), f = __shfl_down(fw, d, 64);
     if (lane + d < 64 && f == fw) grp |= v;
   }
-  const uint32_t gnext = __shfl_down(grp, 1, 64), fnext = __shfl_down(fw, 1, 64);
+  // lane + 1's values (DPP wave_shl:1; lane 63 reads the old 0 / ~0u)
+  const uint32_t gnext = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)grp, 0x130, 0xf, 0xf, false);
+  const uint32_t fnext = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)fw, 0x130, 0xf, 0xf, false);
   if (has && MJG_ABLATE != 4) {
     if (lw > fw) slot[lw] = tail | ((lane < 63 && fnext == lw) ? gnext : 0u);
     if (sft == 0) slot[fw] = grp;  // word-aligned start: this lane opens word fw
@@ -1327,7 +1341,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan_arr(const uint32_t *in, uint3
     const uint32_t v = i < n ? in[i] : 0u;
     const uint32_t incl = wave_incl_scan(v, lane);
     if (i < n) out[i] = carry + incl - v;
-    carry += __shfl(incl, 63, 64);
+    carry += lane63(incl);
   }
   return carry;
 }
@@ -1527,7 +1541,7 @@ __global__ __launch_bounds__(64) void k_seg_sizes(const uint64_t *__restrict__ s
     const uint32_t v = s < nseg ? (uint32_t)seg_size[(size_t)f * nseg + s] : 0u;
     const uint32_t incl = wave_incl_scan(v, lane);
     if (s < nseg) seg_off[(size_t)f * nseg + s] = carry + incl - v;
-    carry += __shfl(incl, 63, 64);
+    carry += lane63(incl);
   }
   if (lane == 0) frame_size[f] = (uint64_t)hdr_len + carry;
 }
@@ -1648,7 +1662,7 @@ __global__ __launch_bounds__(256) void k_write(
           }
         }
       }
-      carry += __shfl(incl, 63, 64);
+      carry += lane63(incl);
     }
   }
 }
