@@ -453,6 +453,9 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
+#ifndef MJG_GRP_SCAN
+#define MJG_GRP_SCAN 1  // pack_chunk group ORs by prefix sum + one bpermute (0: 4-step shuffle OR)
+#endif
 #ifndef MJG_ENC_BATCH
 #define MJG_ENC_BATCH 16
 #endif
@@ -551,6 +554,19 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
       }
     }
   }
+#if MJG_GRP_SCAN
+  // Group OR of the heads of the lanes that start inside word fw, needed at the group's
+  // first lane.  Heads of one word occupy disjoint bits, so their OR is their sum: with H
+  // the inclusive prefix sum of the heads (mod 2^32), the group's OR is H[last] - H[first]
+  // + head[first].  The group's last lane is the lane before the next group's first one
+  // (ballot of the group starts; lane 63 when none follows): one bpermute.
+  const uint32_t fprev = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)fw, 0x138, 0xf, 0xf, false);  // wave_shr:1
+  const uint64_t firsts = __ballot(fprev != fw);
+  const uint64_t later = lane < 63 ? firsts >> (lane + 1) : 0ull;
+  const int last = later ? lane + (int)__builtin_ctzll(later) : 63;
+  const uint32_t H = wave_incl_scan(head, lane);
+  const uint32_t grp = (uint32_t)__builtin_amdgcn_ds_bpermute(last << 2, (int)H) - H + head;  // valid at group firsts
+#else
   // Every active block is at least 2 bits (a DC code and an EOB or coefficient-63 code,
   // each >= 1 bit), so at most 16 active lanes start inside one word: distances 1..15
   // (steps 1, 2, 4, 8) reach the whole group.  Inactive lanes (the chunk's tail) add 0.
@@ -560,6 +576,7 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
     const uint32_t v = __shfl_down(grp, d, 64), f = __shfl_down(fw, d, 64);
     if (lane + d < 64 && f == fw) grp |= v;
   }
+#endif
   // lane + 1's values (DPP wave_shl:1; lane 63 reads the old 0 / ~0u)
   const uint32_t gnext = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)grp, 0x130, 0xf, 0xf, false);
   const uint32_t fnext = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)fw, 0x130, 0xf, 0xf, false);
@@ -936,7 +953,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // else the carried DCs of the previous chunk.
     const int delta = desc_delta(dsc);
     const int src_lane = (lane - delta) & 63;
-    const int from_cur = __shfl(dc, src_lane, 64), from_prev = __shfl(carry, src_lane, 64);
+    // one bpermute for both: quantised DCs and carried DCs fit int16
+    const uint32_t both = __builtin_amdgcn_ds_bpermute(
+        src_lane << 2, (int)(((uint32_t)dc & 0xffffu) | ((uint32_t)carry << 16)));
+    const int from_cur = (int)(int16_t)(both & 0xffffu), from_prev = (int)both >> 16;
     const int pred = lane >= delta ? from_cur : (cur_chunk == 0 ? 128 : from_prev);
     const int diff = dc - pred;
     carry = dc;
