@@ -288,7 +288,9 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
 
 
 def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(prog="ffmpeg_distributed_amd.worker", add_help=True)
+    # no -h/--help and no abbreviations: every other argument is ffmpeg's (remote_args), and
+    # argparse would read `-huffman default` as `-h uffman`
+    ap = argparse.ArgumentParser(prog="ffmpeg_distributed_amd.worker", add_help=False, allow_abbrev=False)
     ap.add_argument("--device", type=int, required=True)
     ns, rest = ap.parse_known_args(argv)
     try:

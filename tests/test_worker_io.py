@@ -313,3 +313,18 @@ def test_mkv_without_display_size_means_square_pixels():
     w.write_frame(b"x")
     w.close()
     assert container.MkvReader(io.BytesIO(buf.getvalue())).info(1).sar == (1, 1)
+
+
+@pytest.mark.parametrize("args", [
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
+    "-vf scale=1920:1080:flags=bicubic -c:v mjpeg -q:v 3 -dct int -huffman optimal -bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -h -hide_banner --help -devi 1",
+])
+def test_worker_cli_passes_every_ffmpeg_argument(args, monkeypatch):
+    """`python -m ffmpeg_distributed_amd.worker --device N <remote_args>` (the dispatcher's
+    gpu:N argv) hands remote_args to run() unchanged: -huffman is not argparse's -h, and
+    no prefix of --device is taken as --device."""
+    seen = {}
+    monkeypatch.setattr(worker, "run", lambda dev, rest: seen.update(dev=dev, rest=rest) or 0)
+    assert worker.main(["--device", "3", *args.split()]) == 0
+    assert seen == {"dev": 3, "rest": args.split()}
