@@ -222,6 +222,9 @@ class MkvReader:
             self._eof = True
             return False
         size, _ = _read_vint(self.f, False)
+        return self._element(eid, size)
+
+    def _element(self, eid: int, size) -> bool:
         if eid in MASTERS:
             if eid == TRACK_ENTRY:
                 self._in_track = MkvTrack()
@@ -267,6 +270,62 @@ class MkvReader:
         elif eid == 0x55B9 and tr:
             tr.colour_range = int.from_bytes(data, "big")
         return True
+
+    def read_frame_into(self, track: int, dest) -> Optional[int]:
+        """The next block of `track` read straight into `dest` (a writable buffer of exactly
+        the block's payload size: one copy, no intermediate bytes); returns its timestamp
+        (timescale units), or None at the end of the stream."""
+        while True:
+            while self._pending:
+                tn, ts, data = self._pending.pop(0)
+                if tn == track:
+                    if len(data) != len(dest):
+                        raise ValueError(f"frame of {len(data)} bytes, expected {len(dest)}")
+                    dest[:] = data
+                    return ts
+            if self._eof:
+                return None
+            eid, _ = _read_vint(self.f, True)
+            if eid is None:
+                self._eof = True
+                return None
+            size, _ = _read_vint(self.f, False)
+            if eid not in (SIMPLE_BLOCK, BLOCK) or size is UNKNOWN:
+                if not self._element(eid, size):
+                    return None
+                continue
+            self._in_track = None
+            first = self.f.read(1)
+            if not first:
+                self._eof = True
+                return None
+            vlen = 1
+            while vlen <= 8 and not first[0] & (0x80 >> (vlen - 1)):
+                vlen += 1
+            rest = self.f.read(vlen - 1 + 3)
+            if len(rest) != vlen + 2:
+                self._eof = True
+                return None
+            tn, _ = _vint_from(first + rest, 0)
+            rel = struct.unpack(">h", rest[vlen - 1:vlen + 1])[0]
+            if rest[vlen + 1] & 0x06:
+                raise ValueError("laced Matroska blocks are not supported")
+            payload = size - vlen - 3
+            if tn != track:
+                if len(self.f.read(payload)) != payload:
+                    self._eof = True
+                    return None
+                continue
+            if payload != len(dest):
+                raise ValueError(f"frame of {payload} bytes, expected {len(dest)}")
+            if self.f.readinto(dest) != payload:
+                self._eof = True
+                return None
+            return self._cluster_ts + rel
+
+    def stop_recording(self) -> None:
+        """No decoder child will need the bytes read so far (raw frames are read natively)."""
+        self._raw.recorded = None
 
     def replay_bytes(self) -> bytes:
         """Every byte taken from the underlying stream so far (record=True), so a
@@ -335,6 +394,8 @@ class _Prefixed:
                 self.recorded += self.head[:n]
             self.head = self.head[n:]
             return n
+        if self.recorded is None and hasattr(self.f, "readinto"):
+            return self.f.readinto(b)  # straight into the caller's buffer
         data = self.f.read(len(b))
         b[:len(data)] = data
         if self.recorded is not None:

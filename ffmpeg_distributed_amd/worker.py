@@ -99,7 +99,8 @@ class Source:
         info = mkv.info(tr.number)
         if tr.codec == "V_UNCOMPRESSED" and tr.colour_space in container.MKV_FOURCC_CHROMA:
             self.info = info
-            self._frames = mkv.frames(tr.number)
+            mkv.stop_recording()
+            self._mkv, self._track = mkv, tr.number
             self.read_into = self._read_mkv
             return
         # any other codec: ffmpeg decodes, we read its y4m
@@ -134,12 +135,11 @@ class Source:
         mv = memoryview(buf).cast("B")
         for i in range(n):
             try:
-                _, data = next(self._frames)
-            except StopIteration:
+                ts = self._mkv.read_frame_into(self._track, mv[i * fb:(i + 1) * fb])
+            except ValueError as e:
+                raise ValueError(f"V_UNCOMPRESSED {e}") from None
+            if ts is None:
                 return i
-            if len(data) != fb:
-                raise ValueError(f"V_UNCOMPRESSED frame of {len(data)} bytes, expected {fb}")
-            mv[i * fb:(i + 1) * fb] = data
         return n
 
     def close(self) -> int:

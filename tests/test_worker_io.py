@@ -328,3 +328,38 @@ def test_worker_cli_passes_every_ffmpeg_argument(args, monkeypatch):
     monkeypatch.setattr(worker, "run", lambda dev, rest: seen.update(dev=dev, rest=rest) or 0)
     assert worker.main(["--device", "3", *args.split()]) == 0
     assert seen == {"dev": 3, "rest": args.split()}
+
+
+def test_source_reads_raw_mkv_frames_in_place():
+    """Raw V_UNCOMPRESSED segments go from the stream straight into the page-locked batch
+    buffer (MkvReader.read_frame_into): same frames as the block iterator, across clusters
+    and a ragged last batch; a wrong-sized block is an error, not a silent truncation."""
+    w, h, n = 48, 32, 70   # 30 fps: three 1 s clusters
+    frames = [np.random.default_rng(i).integers(0, 256, w * h * 3 // 2, dtype=np.uint8) for i in range(n)]
+    buf = io.BytesIO()
+    wr = container.MkvWriter(buf, w, h, Fraction(30), codec="V_UNCOMPRESSED", colour_space=b"I420")
+    for f in frames:
+        wr.write_frame(f.tobytes())
+    wr.close()
+    data = buf.getvalue()
+    src = worker.Source(io.BytesIO(data))
+    assert src._mkv._raw.recorded is None  # no copy of the input kept for a decoder
+    fb = src.info.frame_bytes
+    out = np.zeros((16, fb), np.uint8)
+    got = []
+    while True:
+        k = src.read_into(out, 16)
+        got += [out[i].copy() for i in range(k)]
+        if k < 16:
+            break
+    assert len(got) == n and all((a == b).all() for a, b in zip(got, frames))
+    ref = [d for _, d in container.MkvReader(io.BytesIO(data)).frames(1)]
+    assert [bytes(g) for g in got] == ref
+
+    bad = io.BytesIO()
+    wr = container.MkvWriter(bad, w, h, Fraction(30), codec="V_UNCOMPRESSED", colour_space=b"I420")
+    wr.write_frame(frames[0].tobytes()[:-1])
+    wr.close()
+    src = worker.Source(io.BytesIO(bad.getvalue()))
+    with pytest.raises(ValueError, match="V_UNCOMPRESSED frame of"):
+        src.read_into(np.zeros((1, fb), np.uint8), 1)
