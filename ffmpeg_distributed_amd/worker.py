@@ -31,7 +31,11 @@ from . import container, profile
 
 DECODE_ARGV = ["ffmpeg", "-v", "error", "-f", "matroska", "-i", "pipe:", "-map", "0:v:0",
                "-f", "yuv4mpegpipe", "-strict", "-1", "pipe:"]
-BATCH = int(os.environ.get("MJG_WORKER_BATCH", "32"))
+# frames per submit: MJG_WORKER_BATCH, or as many as fit BATCH_BYTES of input (at most 32).
+# The three page-locked batch buffers are allocated per segment process, and pinning is a
+# large part of its start-up: 4K batches of 32 frames pinned 1.2 GB, of 8 frames 0.3 GB.
+BATCH = int(os.environ.get("MJG_WORKER_BATCH", "0"))
+BATCH_BYTES = int(os.environ.get("MJG_WORKER_BATCH_BYTES", str(96 << 20)))
 # FFmpeg builds differ in the pix_fmt their CLI hands the mjpeg encoder for yuv420p input
 # (yuvj420p: no COM; yuv420p + full range: COM "CS=ITU601"); default = yuvj420p.
 COM_ITU601 = os.environ.get("MJG_COM_ITU601", "0") == "1"
@@ -206,9 +210,11 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     dst_w, dst_h = prof.scale or (info.width, info.height)
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
+    batch = BATCH or max(1, min(32, BATCH_BYTES // max(info.frame_bytes, 1)))
+
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
-                       qscale=prof.qscale, sar=sar, max_batch=BATCH,
+                       qscale=prof.qscale, sar=sar, max_batch=batch,
                        com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman,
                        chroma=info.chroma, rst=prof.rst)
     prog = Progress(stderr, info.fps, prof.qscale)
@@ -220,7 +226,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     # back); a batch returns to the reader once its submit is synced.
     fb = enc.frame_bytes
     nbuf = 3
-    bufs = [PinnedBuffer(BATCH * fb) for _ in range(nbuf)]
+    bufs = [PinnedBuffer(batch * fb) for _ in range(nbuf)]
     free: "queue.Queue[int]" = queue.Queue()
     full: "queue.Queue" = queue.Queue()
     for i in range(nbuf):
@@ -232,9 +238,9 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
                 i = free.get()
                 if i < 0:
                     return
-                n = src.read_into(bufs[i].array, BATCH)
+                n = src.read_into(bufs[i].array, batch)
                 full.put((i, n))
-                if n < BATCH:
+                if n < batch:
                     full.put(None)
                     return
         except BaseException as e:   # surfaced by the main loop
