@@ -151,13 +151,82 @@ def worker_argv(host: str, ffmpeg_args: List[str]) -> List[str]:
     return cmd
 
 
+def server_argv(host: str, ffmpeg_args: List[str]) -> List[str]:
+    """The persistent worker for a gpu:N host (--persistent-gpu-workers): worker.serve."""
+    return worker_argv(host, ffmpeg_args) + ["--serve"]
+
+
+SERVE_DONE = "mjg-serve: segment done rc="
+
+
+class GpuServer:
+    """One long-lived `worker --serve` process per gpu:N TaskThread.  run_task hands it one
+    segment (a request line with the input and output paths) and follows its stderr like
+    FFMPEGProc follows a per-segment worker, up to the segment's done line; its exit code is
+    the segment's.  A server that dies fails the segment (re-queued by the caller, as for a
+    failed per-segment worker) and is started again for the next one."""
+
+    def __init__(self, host: str):
+        self.host = host
+        self.proc: Optional[subprocess.Popen] = None
+        self.args: Optional[List[str]] = None
+        self.stderr = ""
+        self.duration: Optional[float] = None
+
+    def _start(self, ffmpeg_args: List[str]):
+        self.close()
+        self.args = list(ffmpeg_args)
+        self.proc = subprocess.Popen(server_argv(self.host, ffmpeg_args), stdin=subprocess.PIPE,
+                                     stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                     universal_newlines=True, bufsize=1)
+
+    def run_task(self, task: "Task", update_callback: Optional[Callable] = None) -> int:
+        if self.proc is None or self.proc.poll() is not None or self.args != list(task.ffmpeg_args):
+            self._start(task.ffmpeg_args)
+        self.stderr, self.duration = "", None
+        try:
+            self.proc.stdin.write(f"{os.path.abspath(task.input_file)}\t{os.path.abspath(task.output_file)}\n")
+            self.proc.stdin.flush()
+        except (BrokenPipeError, OSError):
+            self.stderr = f"{self.host}: worker server is gone\n"
+            self.close()
+            return 1
+        for line in self.proc.stderr:
+            if line.startswith(SERVE_DONE):
+                return int(line[len(SERVE_DONE):].strip() or 1)
+            prog = parse_progress(line)
+            if prog is None:
+                self.stderr += line
+                if self.duration is None:
+                    self.duration = parse_duration(line)
+            elif update_callback:
+                frame, fps, t, speed = prog
+                update_callback(frame, fps, t, self.duration, speed)
+        rc = self.proc.wait()
+        self.stderr += f"{self.host}: worker server exited with {rc}\n"
+        self.proc = None
+        return rc or 1
+
+    def close(self):
+        if self.proc is not None:
+            try:
+                self.proc.stdin.close()
+            except OSError:
+                pass
+            self.proc.wait()
+            self.proc = None
+
+
 class TaskThread(threading.Thread):
     """One consumer per -H entry: pulls segments until the queue is empty and re-queues
     any segment whose worker exits nonzero (fd.py:105-148)."""
 
-    def __init__(self, host: str, task_queue: "queue.SimpleQueue[Task]", bar_pos: int = 0):
+    def __init__(self, host: str, task_queue: "queue.SimpleQueue[Task]", bar_pos: int = 0,
+                 persistent: bool = False):
         super().__init__(daemon=True)
         self.host = host
+        # gpu:N with --persistent-gpu-workers: segments go to one long-lived worker
+        self.server = GpuServer(host) if persistent and GPU_HOST.match(host) else None
         self.tasks = task_queue
         self.bar = _bar(host, bar_pos)
         self.current = None
@@ -183,17 +252,24 @@ class TaskThread(threading.Thread):
             except queue.Empty:
                 break
             self.current = os.path.basename(task.input_file)
-            with open(task.input_file, "rb") as src, open(task.output_file, "wb") as dst:
-                self._proc = FFMPEGProc(worker_argv(self.host, task.ffmpeg_args), stdin=src,
-                                        stdout=dst, update_callback=self._progress)
-                rc = self._proc.run()
+            if self.server is not None:
+                rc = self.server.run_task(task, self._progress)
+                err = self.server.stderr
+            else:
+                with open(task.input_file, "rb") as src, open(task.output_file, "wb") as dst:
+                    self._proc = FFMPEGProc(worker_argv(self.host, task.ffmpeg_args), stdin=src,
+                                            stdout=dst, update_callback=self._progress)
+                    rc = self._proc.run()
+                err = self._proc.stderr
             if rc != 0:
                 self.failures += 1
                 _report(f"task for {self.current} failed on host {self.host}")
-                _report(self._proc.stderr)
+                _report(err)
                 self.tasks.put(task)
             else:
                 self.done.append(task.input_file)
+        if self.server is not None:
+            self.server.close()
         if self.bar is not None:
             self.bar.close()
 
@@ -222,7 +298,8 @@ def _run_local(argv, desc) -> FFMPEGProc:
 
 def encode(hosts: List[str], input_file: str, output_file: str, segment_seconds: float = 60,
            remote_args: str = "", concat_args: str = "", tmp_dir: Optional[str] = None,
-           keep_tmp: bool = False, resume: bool = False, copy_input: bool = False):
+           keep_tmp: bool = False, resume: bool = False, copy_input: bool = False,
+           persistent_gpu_workers: bool = False):
     """Split -> distributed per-segment encode -> concat (fd.py:150-236)."""
     input_file = os.path.abspath(os.path.expanduser(input_file))
     output_file = os.path.abspath(os.path.expanduser(output_file))
@@ -249,7 +326,7 @@ def encode(hosts: List[str], input_file: str, output_file: str, segment_seconds:
         if not os.path.isfile(out):
             tasks.put(Task(seg, out, list(args)))
 
-    threads = [TaskThread(h, tasks, pos) for pos, h in enumerate(hosts)]
+    threads = [TaskThread(h, tasks, pos, persistent_gpu_workers) for pos, h in enumerate(hosts)]
 
     def on_sigint(sig, frame):
         print("Got SIGINT, stopping...")
@@ -303,6 +380,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-c", "--copy-input", action="store_true",
                    help="Don't (losslessly) re-encode input while segmenting. Only use this if your "
                         'input segments frame-perfectly with "-c:v copy" (i.e. it has no B-frames)')
+    p.add_argument("-P", "--persistent-gpu-workers", action="store_true",
+                   help="gpu:N hosts: one long-lived worker per -H entry encodes every segment it "
+                        "pulls (no per-segment process start, HIP init and buffer allocation).")
     return p
 
 
@@ -310,7 +390,8 @@ def main(argv=None):
     a = build_parser().parse_args(argv)
     encode(a.host, a.input_file, a.output_file, segment_seconds=a.segment_length,
            remote_args=a.remote_args, concat_args=a.concat_args, tmp_dir=a.tmp_dir,
-           keep_tmp=a.keep_tmp, resume=a.resume, copy_input=a.copy_input)
+           keep_tmp=a.keep_tmp, resume=a.resume, copy_input=a.copy_input,
+           persistent_gpu_workers=a.persistent_gpu_workers)
 
 
 if __name__ == "__main__":

@@ -153,10 +153,18 @@ class Source:
         return self.child.wait()
 
 
-def passthrough(args: List[str]) -> int:
-    """Outside the GPU profile: run exactly what the reference runs."""
+def _fd_or_none(f):
     try:
-        return subprocess.call(reference_argv(args))
+        return f.fileno()
+    except (AttributeError, OSError, ValueError):
+        return None
+
+
+def passthrough(args: List[str], stdin=None, stdout=None) -> int:
+    """Outside the GPU profile: run exactly what the reference runs (on this segment's
+    input and output files: the process's own stdin/stdout unless given)."""
+    try:
+        return subprocess.call(reference_argv(args), stdin=_fd_or_none(stdin), stdout=_fd_or_none(stdout))
     except FileNotFoundError:
         sys.stderr.write("ffmpeg not found for a non-GPU profile\n")
         return 127
@@ -190,7 +198,9 @@ def ffmpeg_fallthrough(src: Source, args: List[str], stdout) -> int:
     return rc or src.close()
 
 
-def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> int:
+def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cache=None) -> int:
+    """One segment, stdin -> stdout.  `cache` (serve mode): a dict that keeps the encoder
+    context and the page-locked batch buffers between segments of the same stream shape."""
     stdin = stdin or sys.stdin.buffer
     stdout = stdout or sys.stdout.buffer
     stderr = stderr or sys.stderr
@@ -198,7 +208,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     if prof is None:
         stderr.write(f"gpu:{device}: {why}; running ffmpeg on the CPU\n")
         stderr.flush()
-        return passthrough(args)
+        return passthrough(args, stdin, stdout)
 
     src = Source(stdin)
     info = src.info
@@ -213,10 +223,21 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     batch = BATCH or max(1, min(32, BATCH_BYTES // max(info.frame_bytes, 1)))
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
-    enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
-                       qscale=prof.qscale, sar=sar, max_batch=batch,
-                       com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman,
-                       chroma=info.chroma, rst=prof.rst)
+    key = (info.width, info.height, dst_w, dst_h, info.full_range, prof.qscale, sar,
+           COM_ITU601 and not info.full_range, prof.huffman, info.chroma, prof.rst, batch)
+    nbuf = 3
+    if cache is not None and cache.get("key") == key:
+        enc, bufs = cache["enc"], cache["bufs"]
+    else:
+        if cache is not None:
+            release(cache)
+        enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
+                           qscale=prof.qscale, sar=sar, max_batch=batch,
+                           com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman,
+                           chroma=info.chroma, rst=prof.rst)
+        bufs = [PinnedBuffer(batch * enc.frame_bytes) for _ in range(nbuf)]
+        if cache is not None:
+            cache.update(key=key, enc=enc, bufs=bufs)
     prog = Progress(stderr, info.fps, prof.qscale)
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)
@@ -225,8 +246,6 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
     # encoder takes a second submit before the first is synced, so its kernels run back to
     # back); a batch returns to the reader once its submit is synced.
     fb = enc.frame_bytes
-    nbuf = 3
-    bufs = [PinnedBuffer(batch * fb) for _ in range(nbuf)]
     free: "queue.Queue[int]" = queue.Queue()
     full: "queue.Queue" = queue.Queue()
     for i in range(nbuf):
@@ -281,15 +300,65 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None) -> i
             drain_one()
         mkv.close()
         prog.update(frames, 0, final=True)
+    except BaseException:
+        if cache is not None:  # a submit may still be queued: start the next segment afresh
+            cache.pop("key", None)
+            cache.pop("enc", None)
+            cache.pop("bufs", None)
+            cache = None
+        raise
     finally:
         free.put(-1)
-        enc.close()
-        for b in bufs:
-            b.free()
+        if cache is None:
+            enc.close()
+            for b in bufs:
+                b.free()
     rc = src.close()
     if rc:
         stderr.write(f"decoder exited with {rc}\n")
         return 1
+    return 0
+
+
+def release(cache) -> None:
+    """Close the encoder context and free the batch buffers a serve cache holds."""
+    enc, bufs = cache.pop("enc", None), cache.pop("bufs", None) or []
+    cache.pop("key", None)
+    if enc is not None:
+        enc.close()
+    for b in bufs:
+        b.free()
+
+
+SERVE_DONE = "mjg-serve: segment done rc="
+
+
+def serve(device: int, args: List[str], requests=None, stderr=None) -> int:
+    """Persistent worker (dispatcher --persistent-gpu-workers): one process per `-H gpu:N`
+    entry encodes segment after segment, keeping its HIP context, encoder and page-locked
+    buffers, so a segment no longer pays process start + HIP init + allocation (~0.5 s).
+    Each request line on stdin is `INPUT<TAB>OUTPUT`; the segment runs exactly as `run`
+    runs it for one process (same output bytes, same ffmpeg-style stderr lines), then
+    `mjg-serve: segment done rc=N` on stderr ends it.  EOF on stdin ends the server."""
+    requests = requests or sys.stdin
+    stderr = stderr or sys.stderr
+    cache: dict = {}
+    try:
+        for line in requests:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            try:
+                src, dst = line.split("\t")
+                with open(src, "rb") as fin, open(dst, "wb") as fout:
+                    rc = run(device, args, stdin=fin, stdout=fout, stderr=stderr, cache=cache)
+            except Exception as e:
+                stderr.write(f"gpu:{device}: {type(e).__name__}: {e}\n")
+                rc = 1
+            stderr.write(f"{SERVE_DONE}{rc}\n")
+            stderr.flush()
+    finally:
+        release(cache)
     return 0
 
 
@@ -298,7 +367,10 @@ def main(argv=None) -> int:
     # argparse would read `-huffman default` as `-h uffman`
     ap = argparse.ArgumentParser(prog="ffmpeg_distributed_amd.worker", add_help=False, allow_abbrev=False)
     ap.add_argument("--device", type=int, required=True)
+    ap.add_argument("--serve", action="store_true")
     ns, rest = ap.parse_known_args(argv)
+    if ns.serve:
+        return serve(ns.device, rest)
     try:
         return run(ns.device, rest)
     except Exception as e:  # the dispatcher re-queues the segment on a nonzero exit

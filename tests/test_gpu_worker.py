@@ -118,3 +118,28 @@ def test_worker_raw_mkv_422_444_rst(fourcc, chroma, extra, monkeypatch):
         y, u, v = split_i420(f, w, h, chroma)
         ref = oracle.encode_frame(y, u, v, full_range=False, qscale=q, sar=(1, 1), chroma=chroma, rst=True)
         assert packets[i] == ref, f"frame {i}"
+
+
+def test_worker_serve_reuses_context_across_segments(tmp_path):
+    """worker.serve (dispatcher -P): segments of one shape share the encoder context and
+    batch buffers, a segment of another shape gets a new one; every packet still equals
+    the oracle's encode of its frame."""
+    segs = [(96, 64, 5, 3), (96, 64, 5, 9), (80, 48, 5, 4), (96, 64, 5, 2)]
+    reqs, want = [], []
+    for i, (w, h, q, n) in enumerate(segs):
+        frames = [make_testsrc(w, h, 11 * i + k) for k in range(n)]
+        buf = io.BytesIO()
+        wr = container.MkvWriter(buf, w, h, Fraction(25), codec="V_UNCOMPRESSED", colour_space=b"I420")
+        for f in frames:
+            wr.write_frame(f.tobytes())
+        wr.close()
+        (tmp_path / f"in{i}.mkv").write_bytes(buf.getvalue())
+        reqs.append(f"{tmp_path}/in{i}.mkv\t{tmp_path}/out{i}.mkv\n")
+        want.append([oracle.encode_frame(*split_i420(f, w, h), full_range=False, qscale=q, sar=(1, 1))
+                     for f in frames])
+    err = io.StringIO()
+    assert worker.serve(0, _args(5), requests=io.StringIO("".join(reqs)), stderr=err) == 0
+    assert err.getvalue().count(worker.SERVE_DONE + "0") == len(segs), err.getvalue()
+    for i in range(len(segs)):
+        r = container.MkvReader(io.BytesIO((tmp_path / f"out{i}.mkv").read_bytes()))
+        assert [d for _, d in r.frames(1)] == want[i], f"segment {i}"

@@ -105,3 +105,95 @@ def test_dispatcher_spreads_segments_over_gpu_hosts(tmp_path, monkeypatch):
     assert all(b.startswith(("GPU0[SEG", "GPU1[SEG")) for b in bodies)
     assert {b[:4] for b in bodies} == {"GPU0", "GPU1"}
     assert (tmp_path / "out.mkv").read_text() == "|".join(bodies)
+
+
+STUB_SERVER = r"""
+import os, sys, time
+dev = sys.argv[sys.argv.index("--device") + 1]
+assert sys.argv[-1] == "--serve"
+with open(os.environ["STUB_LOG"], "a") as log:
+    log.write(f"start {dev}\n")
+for line in sys.stdin:
+    src, dst = line.rstrip("\n").split("\t")
+    data = open(src).read()
+    time.sleep(0.05)
+    if data.startswith("SEG2:") and not os.path.exists("crashed"):
+        open("crashed", "w").close()
+        os._exit(3)                      # the server dies mid-segment
+    rc = 0
+    if data.startswith("SEG4:") and not os.path.exists("failed"):
+        open("failed", "w").close()
+        rc = 1                           # one segment fails, the server lives on
+    else:
+        with open(dst, "w") as f:
+            f.write("GPU" + dev + "[" + data + "]")
+    sys.stderr.write("  Duration: 00:00:02.00, start: 0.000000, bitrate: N/A\n")
+    sys.stderr.write("frame=   50 fps= 25 q=5.0 size=N/A time=00:00:02.00 bitrate=N/A speed=1.00x\n")
+    sys.stderr.write(f"mjg-serve: segment done rc={rc}\n")
+    sys.stderr.flush()
+"""
+
+
+def test_dispatcher_persistent_gpu_workers(tmp_path, monkeypatch):
+    """-P: one long-lived worker per gpu:N entry takes segment after segment over its request
+    pipe; a segment it fails is re-queued like a failed per-segment worker, and a server that
+    dies fails its segment and is started again."""
+    import sys
+    from ffmpeg_distributed_amd import dispatcher as D
+    here = os.path.dirname(os.path.abspath(__file__))
+    monkeypatch.setenv("PATH", os.path.join(here, "shims") + os.pathsep + os.environ["PATH"])
+    monkeypatch.setenv("SHIM_SEGMENTS", "8")
+    monkeypatch.setenv("STUB_LOG", str(tmp_path / "starts.log"))
+    monkeypatch.chdir(tmp_path)
+    stub = tmp_path / "stub_server.py"
+    stub.write_text(STUB_SERVER)
+    real = D.worker_argv
+
+    def argv(host, args):
+        a = real(host, args)
+        assert a[:3] == [sys.executable, "-m", "ffmpeg_distributed_amd.worker"]
+        return [sys.executable, str(stub)] + a[3:]
+
+    monkeypatch.setattr(D, "worker_argv", argv)
+    (tmp_path / "input.mp4").write_text("RAW")
+    D.encode(["gpu:0", "gpu:1"], "input.mp4", "out.mkv", 2, "-c:v mjpeg -q:v 5", "-an",
+             tmp_dir="segs", keep_tmp=True, persistent_gpu_workers=True)
+    outs = sorted(os.listdir(tmp_path / "segs" / "out"))
+    assert outs == [f"{i:08d}.mkv" for i in range(8)]
+    bodies = [(tmp_path / "segs" / "out" / o).read_text() for o in outs]
+    assert all(b.startswith(("GPU0[SEG", "GPU1[SEG")) for b in bodies)
+    assert [b[5:9] for b in bodies] == [f"SEG{i}" for i in range(8)]
+    assert (tmp_path / "out.mkv").read_text() == "|".join(bodies)
+    starts = (tmp_path / "starts.log").read_text().split("\n")[:-1]
+    assert sorted(set(starts)) == ["start 0", "start 1"]
+    assert len(starts) == 3  # one server per host, plus the restart after the crash
+
+
+def test_worker_serve_protocol(tmp_path, monkeypatch):
+    """worker.serve: one request line per segment, the segment's files opened for run(),
+    the done line carries run()'s exit code (an exception is a failed segment, rc 1)."""
+    import io
+    from ffmpeg_distributed_amd import worker
+    calls = []
+
+    def fake_run(dev, args, stdin, stdout, stderr, cache):
+        data = stdin.read()
+        calls.append((dev, args, data, id(cache)))
+        if data == b"boom":
+            raise ValueError("bad segment")
+        stdout.write(b"out:" + data)
+        stderr.write("frame=    1 fps=  1 q=5.0 size=N/A time=00:00:00.04 bitrate=N/A speed=1.00x\n")
+        return 0 if data != b"rc7" else 7
+
+    monkeypatch.setattr(worker, "run", fake_run)
+    reqs = []
+    for i, body in enumerate([b"a", b"boom", b"rc7", b"b"]):
+        (tmp_path / f"in{i}").write_bytes(body)
+        reqs.append(f"{tmp_path}/in{i}\t{tmp_path}/out{i}\n")
+    err = io.StringIO()
+    assert worker.serve(2, ["-q:v", "5"], requests=io.StringIO("".join(reqs)), stderr=err) == 0
+    done = [l for l in err.getvalue().splitlines() if l.startswith(worker.SERVE_DONE)]
+    assert [int(l[len(worker.SERVE_DONE):]) for l in done] == [0, 1, 7, 0]
+    assert "ValueError: bad segment" in err.getvalue()
+    assert (tmp_path / "out0").read_bytes() == b"out:a" and (tmp_path / "out3").read_bytes() == b"out:b"
+    assert len({c[3] for c in calls}) == 1 and all(c[:2] == (2, ["-q:v", "5"]) for c in calls)

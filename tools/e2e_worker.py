@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--seq", type=int, default=3)
     ap.add_argument("--par", type=int, default=2)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--persistent", type=int, default=0,
+                    help="also time this many segments through one `worker --serve` process (dispatcher -P)")
     a = ap.parse_args()
     w, h, fps, args = WORKLOADS[a.workload]
     d = tempfile.mkdtemp(dir=a.dir)
@@ -89,6 +91,26 @@ def main():
         for p in ps:
             finish(p)
         par_s = time.monotonic() - t
+    pers = None
+    if a.persistent:
+        argv = [sys.executable, "-m", "ffmpeg_distributed_amd.worker", "--device", "0", *args, "--serve"]
+        p = subprocess.Popen(argv, stdin=subprocess.PIPE, stderr=subprocess.PIPE, stdout=subprocess.DEVNULL,
+                             universal_newlines=True, bufsize=1, cwd=ROOT)
+        pers = []
+        for i in range(a.persistent):
+            t = time.monotonic()
+            p.stdin.write(f"{seg}\t{os.path.join(d, 'pers.mkv')}\n")
+            p.stdin.flush()
+            for line in p.stderr:
+                if line.startswith("mjg-serve: segment done rc="):
+                    if line.strip()[-2:] != "=0":
+                        raise SystemExit(line)
+                    break
+            else:
+                raise SystemExit("server exited")
+            pers.append(time.monotonic() - t)
+        p.stdin.close()
+        p.wait()
     # an empty segment: process start + HIP init + context, no frames
     empty = os.path.join(d, "empty.mkv")
     make_segment(empty, w, h, fps, 0)
@@ -111,6 +133,9 @@ def main():
         "fps_excluding_startup": round(a.frames / max(best - startup_s, 1e-6), 1),
         "input_gbps_excluding_startup": round(seg_bytes / max(best - startup_s, 1e-6) / 1e9, 2),
         "segment_gen_seconds": round(gen_s, 1),
+        "persistent_seconds": [round(x, 3) for x in pers] if pers else None,
+        "persistent_fps_steady": round(a.frames / (sum(pers[1:]) / (len(pers) - 1)), 1) if pers and len(pers) > 1
+        else None,
     }))
 
 
