@@ -34,13 +34,18 @@ WORKLOADS = {
                                       "-bitexact"]),
     "c4": (3840, 2160, Fraction(60), ["-vf", "scale=1920:1080:flags=bicubic", "-c:v", "mjpeg", "-q:v", "3",
                                       "-dct", "int", "-huffman", "default", "-bitexact"]),
+    # yuvj420p input (Matroska colour range 2: full)
+    "c5": (7680, 4320, Fraction(30), ["-c:v", "mjpeg", "-q:v", "5", "-dct", "int", "-huffman", "default",
+                                      "-bitexact"]),
 }
+FULL_RANGE = {"c5"}
 
 
-def make_segment(path, w, h, fps, frames, distinct=8):
-    pool = [testsrc2_i420(w, h, t).tobytes() for t in range(distinct)]
+def make_segment(path, w, h, fps, frames, distinct=8, full_range=False):
+    pool = [testsrc2_i420(w, h, t, full_range=full_range).tobytes() for t in range(min(distinct, frames))]
     with open(path, "wb") as f:
-        wr = container.MkvWriter(f, w, h, fps, codec="V_UNCOMPRESSED", colour_space=b"I420")
+        wr = container.MkvWriter(f, w, h, fps, codec="V_UNCOMPRESSED", colour_space=b"I420",
+                                 colour_range=2 if full_range else 0)
         for i in range(frames):
             wr.write_frame(pool[i % distinct])
         wr.close()
@@ -73,7 +78,7 @@ def main():
     d = tempfile.mkdtemp(dir=a.dir)
     seg = os.path.join(d, "seg.mkv")
     t0 = time.monotonic()
-    make_segment(seg, w, h, fps, a.frames)
+    make_segment(seg, w, h, fps, a.frames, full_range=a.workload in FULL_RANGE)
     gen_s = time.monotonic() - t0
     seg_bytes = os.path.getsize(seg)
 
@@ -113,7 +118,7 @@ def main():
         p.wait()
     # an empty segment: process start + HIP init + context, no frames
     empty = os.path.join(d, "empty.mkv")
-    make_segment(empty, w, h, fps, 0)
+    make_segment(empty, w, h, fps, 0, full_range=a.workload in FULL_RANGE)
     t = time.monotonic()
     finish(start(empty, os.path.join(d, "empty_out.mkv"), args))
     startup_s = time.monotonic() - t
