@@ -30,6 +30,8 @@ from ffmpeg_distributed_amd.testsrc import testsrc2_i420  # noqa: E402
 
 WORKLOADS = {
     "c1": (1920, 1080, Fraction(30), ["-c:v", "mjpeg", "-q:v", "5", "-dct", "int", "-bitexact"]),
+    "c1d": (1920, 1080, Fraction(30), ["-c:v", "mjpeg", "-q:v", "5", "-dct", "int", "-huffman", "default",
+                                       "-bitexact"]),
     "c2": (3840, 2160, Fraction(60), ["-c:v", "mjpeg", "-q:v", "5", "-dct", "int", "-huffman", "default",
                                       "-bitexact"]),
     "c4": (3840, 2160, Fraction(60), ["-vf", "scale=1920:1080:flags=bicubic", "-c:v", "mjpeg", "-q:v", "3",
