@@ -267,10 +267,15 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
     if (p.hf.pos[i] < p.hf.pos[i - 1]) return set_err(MJG_E_INVALID, "non-monotone hscale");
   for (int i = 1; i < dh; i++)
     if (p.vf.pos[i] < p.vf.pos[i - 1]) return set_err(MJG_E_INVALID, "non-monotone vscale");
-  const int ht = p.hf.taps, vt = p.vf.taps;
-  if ((ht & 3) || (vt & 1)) return set_err(MJG_E_INVALID, "filter taps %d/%d not aligned", ht, vt);
-  for (int i = 0; i < dw; i++)
-    if (p.hf.pos[i] + ht > sw) return set_err(MJG_E_INVALID, "hscale window past the row");
+  // h taps padded with zero coefficients to a multiple of 4 (k_scale takes 4 taps per step),
+  // v taps of any count (the pair table below zero-pads).  A window may run past the row
+  // end (tiny sources, padded taps): initFilter zeroes every coefficient past srcW, so the
+  // bytes k_scale stages there never count.
+  const int ht0 = p.hf.taps, vt = p.vf.taps;
+  const int ht = (ht0 + 3) & ~3;
+  std::vector<int16_t> hpad((size_t)dw * ht, 0);
+  for (int x = 0; x < dw; x++)
+    for (int k = 0; k < ht0; k++) hpad[(size_t)x * ht + k] = p.hf.coeff[(size_t)x * ht0 + k];
   // h: coefficient pairs per output column; v: pairs starting at the even row <= pos[y],
   // shifted by its parity and zero-padded to npv = vt/2 + 1 pairs
   const int npv = vt / 2 + 1;
@@ -282,7 +287,7 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   for (size_t i = 0; i < p.hf.coeff.size(); i++)
     if (p.hf.coeff[i] < -128 * 128 - 64 || p.hf.coeff[i] >= 127 * 128 + 64) p.d4 = false;
   for (int x = 0; x < dw; x++) {
-    const int16_t *cx = &p.hf.coeff[(size_t)x * ht];
+    const int16_t *cx = &hpad[(size_t)x * ht];
     for (int k = 0; k < ht; k++) hsum[x] += cx[k];
     for (int k = 0; k < ht / 2; k++) {
       uint32_t wv;

@@ -192,6 +192,12 @@ def test_output_overflow_regrow():
     (160, 96, 80, 48, True),
     (100, 60, 64, 40, False),
     (64, 48, 100, 70, True),
+    # one axis unscaled: swscale's 1-tap filter (odd v taps; h taps padded to 4 with zeros)
+    (1920, 1080, 1280, 1080, False),
+    (1920, 1080, 1920, 720, True),
+    # sources narrower than the filter: windows past the row end (zeroed coefficients)
+    (9, 8, 30, 8, False),
+    (12, 10, 8, 9, True),
 ])
 def test_scale_matches_oracle(sw, sh, dw, dh, full):
     n = 2
@@ -358,3 +364,45 @@ def test_pipelined_submits():
         enc.sync()
         b = enc.fetch()
     assert a + b == oracle_frames(nz, 256, 128, 2, True)
+
+
+def _sweep_cases(seed=2026, n=600):
+    """Seeded random configurations over every option of the GPU profile at once."""
+    rng = np.random.default_rng(seed)
+    kinds = ["noise", "smooth", "checker", "patches", "testsrc", "flat"]
+    out = []
+    for i in range(n):
+        w, h = int(rng.integers(8, 421)), int(rng.integers(8, 261))
+        chroma = ["420", "422", "444"][int(rng.integers(0, 3))]
+        rst = bool(rng.integers(0, 2))
+        huffman = "default" if rst else ["default", "optimal"][int(rng.integers(0, 2))]
+        scale = None
+        if rng.integers(0, 3) == 0:
+            # downscales up to 4:1 (one k_scale LDS tile), upscales up to 2:1
+            scale = (int(rng.integers(max(8, w // 4), 2 * w + 1)), int(rng.integers(max(8, h // 4), 2 * h + 1)))
+        out.append(dict(w=w, h=h, q=int(rng.integers(1, 32)), full=bool(rng.integers(0, 2)),
+                        kind=kinds[int(rng.integers(0, len(kinds)))], chroma=chroma, rst=rst,
+                        huffman=huffman, scale=scale, n=int(rng.integers(1, 4)),
+                        batch=int(rng.integers(1, 4)), seed=i))
+    return out
+
+
+SWEEP = _sweep_cases()
+
+
+@pytest.mark.parametrize("part", range(12))
+def test_random_sweep_matches_oracle(part):
+    """600 seeded random configurations (size 8..420 x 8..260, q 1..31, tv/pc range, six
+    content kinds, 4:2:0/4:2:2/4:4:4, plain/RST layout, default/optimal tables, up- and
+    down-scaling, ragged batches): every frame byte-identical to the oracle."""
+    for c in SWEEP[part::12]:
+        w, h = c["w"], c["h"]
+        dw, dh = c["scale"] or (None, None)
+        frames = rand_frames(w, h, c["n"], seed=c["seed"], kind=c["kind"], chroma=c["chroma"])
+        with MjpegEncoder(0, w, h, dw, dh, qscale=c["q"], full_range=c["full"], max_batch=c["batch"],
+                          huffman=c["huffman"], chroma=c["chroma"], rst=c["rst"]) as enc:
+            got = enc.encode(frames)
+        ref = oracle_frames(frames, w, h, c["q"], c["full"], dw, dh, huffman=c["huffman"],
+                            chroma=c["chroma"], rst=c["rst"])
+        for i in range(c["n"]):
+            assert got[i] == ref[i], (c, i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
