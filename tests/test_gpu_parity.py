@@ -366,13 +366,13 @@ def test_pipelined_submits():
     assert a + b == oracle_frames(nz, 256, 128, 2, True)
 
 
-def _sweep_cases(seed=2026, n=600):
+def _sweep_cases(seed=2026, n=600, wmax=420, hmax=260, nmax=3):
     """Seeded random configurations over every option of the GPU profile at once."""
     rng = np.random.default_rng(seed)
     kinds = ["noise", "smooth", "checker", "patches", "testsrc", "flat"]
     out = []
     for i in range(n):
-        w, h = int(rng.integers(8, 421)), int(rng.integers(8, 261))
+        w, h = int(rng.integers(8, wmax + 1)), int(rng.integers(8, hmax + 1))
         chroma = ["420", "422", "444"][int(rng.integers(0, 3))]
         rst = bool(rng.integers(0, 2))
         huffman = "default" if rst else ["default", "optimal"][int(rng.integers(0, 2))]
@@ -382,12 +382,13 @@ def _sweep_cases(seed=2026, n=600):
             scale = (int(rng.integers(max(8, w // 4), 2 * w + 1)), int(rng.integers(max(8, h // 4), 2 * h + 1)))
         out.append(dict(w=w, h=h, q=int(rng.integers(1, 32)), full=bool(rng.integers(0, 2)),
                         kind=kinds[int(rng.integers(0, len(kinds)))], chroma=chroma, rst=rst,
-                        huffman=huffman, scale=scale, n=int(rng.integers(1, 4)),
+                        huffman=huffman, scale=scale, n=int(rng.integers(1, nmax + 1)),
                         batch=int(rng.integers(1, 4)), seed=i))
     return out
 
 
 SWEEP = _sweep_cases()
+SWEEP_LARGE = _sweep_cases(seed=7, n=48, wmax=2200, hmax=1300, nmax=1)  # up to past 1080p
 
 
 @pytest.mark.parametrize("part", range(12))
@@ -395,7 +396,17 @@ def test_random_sweep_matches_oracle(part):
     """600 seeded random configurations (size 8..420 x 8..260, q 1..31, tv/pc range, six
     content kinds, 4:2:0/4:2:2/4:4:4, plain/RST layout, default/optimal tables, up- and
     down-scaling, ragged batches): every frame byte-identical to the oracle."""
-    for c in SWEEP[part::12]:
+    _sweep(SWEEP[part::12])
+
+
+@pytest.mark.parametrize("part", range(4))
+def test_random_sweep_large_matches_oracle(part):
+    """48 more seeded random configurations at 8..2200 x 8..1300 (one frame each)."""
+    _sweep(SWEEP_LARGE[part::4])
+
+
+def _sweep(cases):
+    for c in cases:
         w, h = c["w"], c["h"]
         dw, dh = c["scale"] or (None, None)
         frames = rand_frames(w, h, c["n"], seed=c["seed"], kind=c["kind"], chroma=c["chroma"])
