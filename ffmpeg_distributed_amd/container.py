@@ -323,6 +323,64 @@ class MkvReader:
                 return None
             return self._cluster_ts + rel
 
+    def _held(self) -> int:
+        """Bytes this reader holds past its logical position (may refill from the stream)."""
+        return len(self.f.peek(1))
+
+    def frames_into_pread(self, track: int, dests, pread) -> int:
+        """Like read_frame_into over `dests`, for a stream backed by a regular file: block
+        headers are parsed here, each payload is skipped and handed to `pread(file_offset,
+        dest)` (positional reads, which the caller runs in parallel).  Returns how many of
+        `dests` got a block; the caller waits for the reads."""
+        outer = self._raw.f
+        n = 0
+        while n < len(dests):
+            if self._pending:
+                if self.read_frame_into(track, dests[n]) is None:
+                    return n
+                n += 1
+                continue
+            if self._eof:
+                return n
+            eid, _ = _read_vint(self.f, True)
+            if eid is None:
+                self._eof = True
+                return n
+            size, _ = _read_vint(self.f, False)
+            if eid not in (SIMPLE_BLOCK, BLOCK) or size is UNKNOWN:
+                if not self._element(eid, size):
+                    return n
+                continue
+            self._in_track = None
+            first = self.f.read(1)
+            if not first:
+                self._eof = True
+                return n
+            vlen = 1
+            while vlen <= 8 and not first[0] & (0x80 >> (vlen - 1)):
+                vlen += 1
+            rest = self.f.read(vlen - 1 + 3)
+            if len(rest) != vlen + 2:
+                self._eof = True
+                return n
+            tn, _ = _vint_from(first + rest, 0)
+            if rest[vlen + 1] & 0x06:
+                raise ValueError("laced Matroska blocks are not supported")
+            payload = size - vlen - 3
+            if tn == track and payload != len(dests[n]):
+                raise ValueError(f"frame of {payload} bytes, expected {len(dests[n])}")
+            held = self._held()
+            off = outer.tell() - held  # file offset of the payload
+            if payload <= held:
+                self.f.read(payload)
+            else:
+                self.f.read(held)
+                outer.seek(payload - held, 1)
+            if tn == track:
+                pread(off, dests[n])
+                n += 1
+        return n
+
     def stop_recording(self) -> None:
         """No decoder child will need the bytes read so far (raw frames are read natively)."""
         self._raw.recorded = None

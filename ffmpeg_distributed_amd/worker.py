@@ -82,6 +82,31 @@ class Progress:
         self.err.flush()
 
 
+READ_THREADS = int(os.environ.get("MJG_READ_THREADS", "4"))
+
+
+def _regular_file_fd(f) -> Optional[int]:
+    """The descriptor of a seekable regular file behind `f`, else None (pipes, sockets,
+    in-memory streams read sequentially)."""
+    import stat
+    try:
+        fd = f.fileno()
+        if stat.S_ISREG(os.fstat(fd).st_mode) and f.seekable():
+            return fd
+    except (AttributeError, OSError, ValueError):
+        pass
+    return None
+
+
+def _pread_exact(fd: int, dest, off: int) -> None:
+    got = 0
+    while got < len(dest):
+        k = os.preadv(fd, [dest[got:]], off + got)
+        if k <= 0:
+            raise ValueError(f"segment file ends inside a frame at byte {off + got}")
+        got += k
+
+
 class Source:
     """Packed planar frames from stdin: .info (StreamInfo), .read_into(buf, n) -> count."""
 
@@ -106,6 +131,11 @@ class Source:
             mkv.stop_recording()
             self._mkv, self._track = mkv, tr.number
             self.read_into = self._read_mkv
+            self._fd = _regular_file_fd(raw)
+            if self._fd is not None:  # a file (the dispatcher's segment): parallel positional reads
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(READ_THREADS)
+                self.read_into = self._read_mkv_pread
             return
         # any other codec: ffmpeg decodes, we read its y4m
         self.child = subprocess.Popen(DECODE_ARGV, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
@@ -146,7 +176,28 @@ class Source:
                 return i
         return n
 
+    def _read_mkv_pread(self, buf, n):
+        fb = self.info.frame_bytes
+        mv = memoryview(buf).cast("B")
+        futs = []
+
+        def pread(off, dest):
+            futs.append(self._pool.submit(_pread_exact, self._fd, dest, off))
+
+        try:
+            got = self._mkv.frames_into_pread(self._track, [mv[i * fb:(i + 1) * fb] for i in range(n)], pread)
+        except ValueError as e:
+            raise ValueError(f"V_UNCOMPRESSED {e}") from None
+        finally:
+            for f in futs:
+                f.result()
+        return got
+
     def close(self) -> int:
+        pool = getattr(self, "_pool", None)
+        if pool is not None:
+            pool.shutdown()
+            self._pool = None
         if self.child is None:
             return 0
         self.child.stdout.close()

@@ -363,3 +363,43 @@ def test_source_reads_raw_mkv_frames_in_place():
     src = worker.Source(io.BytesIO(bad.getvalue()))
     with pytest.raises(ValueError, match="V_UNCOMPRESSED frame of"):
         src.read_into(np.zeros((1, fb), np.uint8), 1)
+
+
+def test_source_parallel_reads_from_a_file(tmp_path):
+    """A segment that is a regular file (the dispatcher's stdin, or worker --serve): block
+    headers parsed in order, payloads fetched by parallel positional reads into the batch
+    buffer; same frames as the sequential reader, across clusters and ragged batches."""
+    w, h, n = 40, 24, 75
+    frames = [np.random.default_rng(100 + i).integers(0, 256, w * h * 3 // 2, dtype=np.uint8)
+              for i in range(n)]
+    path = tmp_path / "seg.mkv"
+    with open(path, "wb") as f:
+        wr = container.MkvWriter(f, w, h, Fraction(25), codec="V_UNCOMPRESSED", colour_space=b"I420")
+        for fr in frames:
+            wr.write_frame(fr.tobytes())
+        wr.close()
+    for batch in (1, 7, 32):
+        with open(path, "rb") as fin:
+            src = worker.Source(fin)
+            assert src.read_into == src._read_mkv_pread
+            out = np.zeros((batch, src.info.frame_bytes), np.uint8)
+            got = []
+            while True:
+                k = src.read_into(out, batch)
+                got += [out[i].copy() for i in range(k)]
+                if k < batch:
+                    break
+            assert src.close() == 0
+        assert len(got) == n and all((a == b).all() for a, b in zip(got, frames)), batch
+
+    bad = tmp_path / "bad.mkv"
+    with open(bad, "wb") as f:
+        wr = container.MkvWriter(f, w, h, Fraction(25), codec="V_UNCOMPRESSED", colour_space=b"I420")
+        wr.write_frame(frames[0].tobytes())
+        wr.write_frame(frames[1].tobytes()[:-3])
+        wr.close()
+    with open(bad, "rb") as fin:
+        src = worker.Source(fin)
+        with pytest.raises(ValueError, match="V_UNCOMPRESSED frame of"):
+            src.read_into(np.zeros((2, src.info.frame_bytes), np.uint8), 2)
+        src.close()
