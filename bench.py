@@ -3,14 +3,20 @@
 (configs[1]: "4K60 60 s testsrc2 yuv420p MJPEG q=5 on one MI355X").  `--workload` selects
 the other BASELINE configs at their own segment sizes (c1 1080p with FFmpeg's default
 -huffman optimal, c4 4K->1080p bicubic q=3, c5 8K yuvj420p 0.5 s segments); the default
-run (no flags) is configs[1], the line the driver records.
+run (no flags) is configs[1], the line the driver records.  `--content` swaps the
+testsrc2-like frames for fractal "natural" content or testsrc2 with noise macroblocks
+(content sensitivity of the entropy coder).
 
 A step = one 2-second segment (120 frames of 3840x2160 yuv420p) encoded on one GPU,
-frames already resident in HBM (a pool of distinct synthetic testsrc2-like frames
-generated on the device), JPEG output packed in HBM.  Default K=30 steps = the 60 s
-(3600-frame) clip of configs[1].  Multi-GPU: one process per GPU
+frames already resident in HBM (a pool of distinct synthetic frames generated on the
+device), JPEG output packed in HBM.  Multi-GPU: one process per GPU
 (torch.distributed.run), segments sharded with no data-path collective (weak scaling);
 the barrier / max-over-ranks timing uses the process group only for bookkeeping.
+
+Roofline: algorithmic bytes = input planes read + JPEG bytes written; the
+primary `roofline` is the kernel that reads the input planes, `roofline_kernels` lists every
+timed kernel with its own algorithmic bytes and, when profiles/pmc_<workload>.json holds a
+PMC pass of the same configuration, its counted HBM traffic.
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task description).
 """
@@ -18,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -47,6 +54,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    p.add_argument("--content", choices=["testsrc", "natural", "noise-patches"], default="testsrc")
     p.add_argument("--huffman", choices=["default", "optimal"], default=None)
     p.add_argument("--rst", action="store_true",
                    help="slice-threaded layout (-slices N: DRI + one restart interval per MCU row)")
@@ -54,36 +62,41 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--pool", type=int, default=480, help="distinct resident frames per GPU")
     p.add_argument("--seg", type=int, default=None)
-    p.add_argument("--cpu-sample-frames", type=int, default=96)
+    p.add_argument("--cpu-seconds", type=float, default=4.0,
+                   help="CPU baseline: wall seconds per point of the core-count sweep")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
     p.add_argument("--kernel-timing-detail", action="store_true",
                    help="events around every tail kernel too (adds ~10 us idle per event)")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_encode_4k_q5.json"),
-                   help="PMC traffic summary written by tools/pmc_traffic.py")
     return p.parse_args()
 
 
-def cpu_baseline(nframes: int):
-    """Oracle ('port') on the host cores: bounded sample of the same workload."""
-    import multiprocessing as mp
+# ------------------------------------------------------------------------ CPU baseline
+def host_cpu():
+    """Cores this process may use (affinity, capped by the cgroup CPU quota), the machine's
+    CPU count and model."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    ctx = mp.get_context("fork")
-    with ctx.Pool(cores, initializer=_cpu_init) as pool:
-        pool.map(_cpu_warm, range(cores))
-        t0 = time.perf_counter()
-        sizes = pool.map(_cpu_encode, range(nframes))
-        dt = time.perf_counter() - t0
-    return {"value": nframes / dt, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"{nframes} frames {W}x{H}{'->%dx%d' % (DW, DH) if (DW, DH) != (W, H) else ''} "
-                      f"{'yuvj420p' if FULL else 'yuv420p'} q={Q} -huffman {HUFF} (testsrc2-like, 8 distinct), "
-                      f"oracle/mjpeg_oracle.c (C restatement of FFmpeg's mjpeg+swscale path), "
-                      f"{cores} processes, {dt:.1f} s wall",
-            "mean_jpeg_bytes": float(sum(sizes) / len(sizes))}
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"usable": usable, "affinity": aff, "cgroup_quota": quota, "machine_cpus": os.cpu_count(),
+            "model": model}
 
 
 _CPU_FRAMES = None
@@ -93,20 +106,113 @@ def _cpu_init():
     global _CPU_FRAMES
     from ffmpeg_distributed_amd.testsrc import testsrc2_i420
     from ffmpeg_distributed_amd.encoder import split_i420
+    import oracle
+    oracle.lib()
     _CPU_FRAMES = [split_i420(testsrc2_i420(W, H, t, full_range=FULL), W, H) for t in range(0, 8)]
 
 
-def _cpu_warm(_):
+def _cpu_encode_until(args):
+    """Encode frames until the deadline (time.time() seconds); returns (frames, bytes, end)."""
+    deadline, rank = args
     import oracle
-    oracle.lib()
-    return 0
+    n = nbytes = 0
+    while True:
+        y, u, v = _CPU_FRAMES[(rank + n) % len(_CPU_FRAMES)]
+        nbytes += len(oracle.encode_frame(y, u, v, dst_w=DW, dst_h=DH, full_range=FULL, qscale=Q,
+                                          huffman=HUFF))
+        n += 1
+        if time.time() >= deadline:
+            return n, nbytes, time.time()
 
 
-def _cpu_encode(i):
-    import oracle
-    y, u, v = _CPU_FRAMES[i % len(_CPU_FRAMES)]
-    return len(oracle.encode_frame(y, u, v, dst_w=DW, dst_h=DH, full_range=FULL, qscale=Q,
-                                   huffman=HUFF))
+def cpu_baseline(seconds: float):
+    """The oracle (kind "port": the C restatement of FFmpeg's mjpeg + swscale path, scalar
+    C, one frame per process) on this host's cores, swept over process counts
+    K in {1, usable/4, usable/2, usable}; each point runs `seconds` of wall time.  The value
+    is the best point.  FFmpeg itself (the reference CPU path) is absent on this pool."""
+    import multiprocessing as mp
+    hc = host_cpu()
+    ks = sorted({1, max(1, hc["usable"] // 4), max(1, hc["usable"] // 2), hc["usable"]})
+    ctx = mp.get_context("fork")
+    sweep = []
+    with ctx.Pool(hc["usable"], initializer=_cpu_init) as pool:
+        pool.map(time.sleep, [0.01] * hc["usable"])  # every worker initialised
+        for k in ks:
+            t0 = time.time()
+            res = pool.map(_cpu_encode_until, [(t0 + seconds, r) for r in range(k)], chunksize=1)
+            dt = max(e for _, _, e in res) - t0
+            frames = sum(n for n, _, _ in res)
+            sweep.append({"processes": k, "frames": frames, "seconds": round(dt, 2),
+                          "value": round(frames / dt, 2),
+                          "mean_jpeg_bytes": round(sum(b for _, b, _ in res) / max(frames, 1), 1)})
+    best = max(sweep, key=lambda s: s["value"])
+    return {"value": best["value"], "unit": "frames/s", "cores": best["processes"], "kind": "port",
+            "sample": f"{W}x{H}{'->%dx%d' % (DW, DH) if (DW, DH) != (W, H) else ''} "
+                      f"{'yuvj420p' if FULL else 'yuv420p'} q={Q} -huffman {HUFF}, 8 distinct "
+                      f"testsrc2-like frames cycled, {seconds:g} s of wall time per sweep point; "
+                      f"oracle/mjpeg_oracle.c (scalar C restatement of FFmpeg's mjpeg + swscale "
+                      f"path, not FFmpeg's SIMD encoder: FFmpeg is absent on this pool), one frame "
+                      f"per process at a time",
+            "host": hc, "sweep": sweep}
+
+
+# ------------------------------------------------------------------------ roofline
+def frame_bytes(w, h):
+    return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
+
+
+def load_pmc(workload, content):
+    if content != "testsrc":
+        return {}
+    try:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json")) as f:
+            return json.load(f).get("kernels", {})
+    except (OSError, ValueError):
+        return {}
+
+
+def pmc_traffic(pmc, *names):
+    """HBM bytes per launch of the kernels whose names contain any of `names` (None when the
+    PMC file has none of them)."""
+    hit = [v["hbm_bytes_per_launch"] for k, v in pmc.items() if any(n in k for n in names)]
+    return sum(hit) if hit else None
+
+
+def roofline_entry(kernel, alg_bytes, ms, traffic, what):
+    ach = alg_bytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4), "bytes": what}
+
+
+def rooflines(kt, seg, mean_jpeg, pmc, optimal, scaled):
+    """Per-kernel roofline entries (SURVEY §8d bytes) and the primary one (reads the input)."""
+    src_b, dst_b, jpeg_b = frame_bytes(W, H) * seg, frame_bytes(DW, DH) * seg, mean_jpeg * seg
+    out = []
+    if scaled and kt.get("scale", 0) > 0:  # unfused: k_scale writes the scaled planes to HBM
+        out.append(roofline_entry("k_scale", src_b + dst_b, kt["scale"], pmc_traffic(pmc, "k_scale"),
+                                  "source planes read + scaled planes written"))
+        enc_in = dst_b
+    else:
+        enc_in = src_b
+    if optimal:
+        out.append(roofline_entry("k_encode<count> + k_huff_build", enc_in, kt["huff"],
+                                  pmc_traffic(pmc, "k_encode", "k_huff_build"),
+                                  "input planes read (symbol records are not credited)"))
+        out.append(roofline_entry("k_emit_syms", jpeg_b, kt["encode"], pmc_traffic(pmc, "k_emit_syms"),
+                                  "JPEG scan bits written"))
+        primary = roofline_entry("count pass + emission (k_encode<count>, k_huff_build, k_emit_syms)",
+                                 enc_in + jpeg_b, kt["huff"] + kt["encode"],
+                                 pmc_traffic(pmc, "k_encode", "k_huff_build", "k_emit_syms"),
+                                 "input planes read + JPEG written")
+    else:
+        name = "k_encode" if not (scaled and kt.get("scale", 0) == 0) else "k_scale_encode (fused)"
+        out.append(roofline_entry(name, enc_in + jpeg_b, kt["encode"],
+                                  pmc_traffic(pmc, "k_encode", "k_scale_encode"),
+                                  ("scaled" if enc_in == dst_b and scaled else "input") +
+                                  " planes read + JPEG written"))
+        primary = out[0]
+    return primary, out
 
 
 def main():
@@ -115,6 +221,8 @@ def main():
     W, H, DW, DH, Q, SEG, FULL, HUFF, WTEXT = WORKLOADS[a.workload]
     if a.huffman:
         HUFF = a.huffman
+    if a.rst:
+        HUFF = "default"  # slice threading forces the default tables
     if a.seg is None:
         a.seg = SEG
     rank = int(os.environ.get("RANK", 0))
@@ -127,7 +235,7 @@ def main():
     B.build()
     from ffmpeg_distributed_amd.encoder import MjpegEncoder
     from ffmpeg_distributed_amd.shard import max_over_ranks, segments_for_rank, timed_region
-    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    from ffmpeg_distributed_amd.testsrc import CONTENT
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -141,23 +249,20 @@ def main():
 
     # The job is (warmup + steps) x world segments of `seg` frames, split round-robin over
     # ranks (shard.segments_for_rank).  Each rank keeps a resident pool of its first
-    # segments' frames (testsrc2-like, time index = global frame number) and cycles it.
+    # segments' frames (time index = global frame number) and cycles it.
     seg = a.seg
     my_segs = segments_for_rank((a.warmup + a.steps) * world, rank, world)
     nseg_pool = max(1, min(len(my_segs), a.pool // seg))
     pool_n = nseg_pool * seg
-    fb = W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)
-    pool = torch.empty((pool_n, fb), dtype=torch.uint8, device=dev)
+    pool = torch.empty((pool_n, frame_bytes(W, H)), dtype=torch.uint8, device=dev)
+    gen_fn = CONTENT[a.content]
     gen = 20 if W * H <= 3840 * 2160 else 5
     for j in range(nseg_pool):
         for i in range(0, seg, gen):
             k = min(gen, seg - i)
-            pool[j * seg + i: j * seg + i + k] = testsrc2_i420_torch(W, H, my_segs[j] * seg + i, k, dev,
-                                                                     full_range=FULL)
+            pool[j * seg + i: j * seg + i + k] = gen_fn(W, H, my_segs[j] * seg + i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
 
-    if a.rst:
-        HUFF = "default"  # slice threading forces the default tables
     enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg,
                        timing=False if a.no_kernel_timing else ("detail" if a.kernel_timing_detail else True),
                        huffman=HUFF, rst=a.rst)
@@ -193,33 +298,20 @@ def main():
     frames_total = a.steps * seg * world
     value = frames_total / dt
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
-
-    # Roofline of the dominant kernel (k_encode): algorithmic bytes per launch =
-    # (input planes 12,441,600 B at 4K + JPEG bytes written) x frames per launch.
-    # With -vf scale the input planes are the scaled frame's (k_scale reads the source and
-    # writes them; its own line is in kernel_ms_per_step).
-    enc_ms = kt["encode"]
-    efb = DW * DH + 2 * ((DW + 1) // 2) * ((DH + 1) // 2)
-    alg_bytes = (efb + mean_jpeg) * seg
-    achieved = alg_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms > 0 else 0.0
-    traffic = None
-    try:
-        with open(a.pmc) as f:
-            pm = json.load(f)
-        if pm.get("workload", {}).get("frames_per_launch") == seg and a.workload == "c2" and \
-                HUFF == "default" and not a.rst:
-            traffic = pm.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    pmc = load_pmc(a.workload, a.content) if (seg == SEG and not a.rst and HUFF == WORKLOADS[a.workload][7]) else {}
+    primary, per_kernel = rooflines(kt, seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H))
+    primary = dict(primary, launches=nl)
 
     out = None
     if rank == 0:
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(a.cpu_sample_frames)
+                cpu = cpu_baseline(a.cpu_seconds)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"value": None, "error": repr(e)}
+        content = {"testsrc": "testsrc2-like generator", "natural": "fractal (1/f) value noise",
+                   "noise-patches": "testsrc2-like with 1/8 of the macroblocks uniform noise"}[a.content]
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -232,19 +324,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: testsrc2-like generator, frames resident in HBM "
-                    f"({pool_n} distinct per GPU), output packed in HBM",
-            "config": {"workload": WTEXT, "width": W, "height": H, "dst_width": DW,
-                       "dst_height": DH, "qscale": Q, "frames_per_step": seg,
+            "data": f"synthetic: {content}, frames resident in HBM ({pool_n} distinct per GPU), "
+                    "output packed in HBM",
+            "config": {"workload": WTEXT, "content": a.content, "width": W, "height": H,
+                       "dst_width": DW, "dst_height": DH, "qscale": Q, "frames_per_step": seg,
                        "global_batch": seg * world, "parallelism": f"segment-dp{world}",
                        "profile": (f"-vf scale={DW}:{DH}:flags=bicubic " if (DW, DH) != (W, H) else "")
                        + f"-c:v mjpeg -q:v {Q} -dct int -huffman {HUFF} -bitexact"
                        + (" -slices 8" if a.rst else "")},
-            "roofline": {"bound": "hbm", "kernel": "k_encode",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "alg_bytes_per_launch": int(alg_bytes),
-                         "avg_launch_ms": round(enc_ms, 4), "launches": nl},
+            "roofline": primary,
+            "roofline_kernels": per_kernel,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},
             "mean_jpeg_bytes": round(mean_jpeg, 1),
             "cpu_baseline": cpu,

@@ -1,8 +1,16 @@
 """In-tree build of libmjgpu.so (hipcc, gfx950).  The .so stays next to this file so
-it travels to the GPU box with the repo snapshot (it is git-ignored)."""
+it travels to the GPU box with the repo snapshot (it is git-ignored).
+
+Staleness is decided by content, not mtime: a sidecar `libmjgpu.so.sha256` records the
+SHA-256 of every source, header and the compile command the library was built from, and
+build() recompiles whenever that digest differs (or the library or its sidecar is missing).
+A pushed binary whose sources changed is therefore always rebuilt where a compiler exists;
+where none exists (a box without hipcc), `check()` reports the mismatch."""
 from __future__ import annotations
 
+import hashlib
 import os
+import shutil
 import subprocess
 import sys
 
@@ -10,33 +18,56 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libmjgpu.so")
+STAMP = LIB + ".sha256"
 SOURCES = ["api.hip", "sws_filter.cpp"]
-DEPS = SOURCES + ["kernels.hip", "scale.hip", "jpeg_tables.h", "sws_filter.h"]
+DEPS = SOURCES + ["kernels.hip", "scale.hip", "fused.hip", "jpeg_tables.h", "sws_filter.h"]
 ARCH = os.environ.get("MJG_OFFLOAD_ARCH", "gfx950")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "mjgpu.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
-
-
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
+def _command(out: str):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     # -fno-slp-vectorize: the SLP vectoriser packs k_encode's per-column fp32 chains into
     # v_pk_fma_f32 across columns, which doubles live registers (123 VGPRs -> 168 + 180 B
     # of scratch spills per lane) and costs ~30% of k_encode time.
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+           "-I", os.path.join(ROOT, "include"), "-o", out]
+    return cmd + [os.path.join(CSRC, s) for s in SOURCES]
+
+
+def source_digest() -> str:
+    """SHA-256 over the sources, the public header and the compile flags."""
+    h = hashlib.sha256()
+    paths = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(ROOT, "include", "mjgpu.h")]
+    for p in paths:
+        if not os.path.exists(p):
+            continue
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(_command("OUT")[1:]).replace(ROOT, "ROOT").encode())
+    return h.hexdigest()
+
+
+def check() -> bool:
+    """True when libmjgpu.so exists and was built from the current sources."""
+    if not os.path.exists(LIB) or not os.path.exists(STAMP):
+        return False
+    with open(STAMP) as f:
+        return f.read().strip() == source_digest()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and check():
+        return LIB
+    cmd = _command(LIB + ".tmp")
+    if not shutil.which(cmd[0]) and not os.path.exists(cmd[0]):
+        raise RuntimeError(f"{LIB} is missing or stale (sources changed) and {cmd[0]} is absent")
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(LIB + ".tmp", LIB)
+    with open(STAMP, "w") as f:
+        f.write(source_digest() + "\n")
     return LIB
 
 

@@ -205,7 +205,6 @@ struct mjg_ctx {
   uint32_t *d_stage_bits = nullptr;  // k_encode: per wave, lane-major staging of blocks past 128 bits
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
-  bool reencode = false;       // optimal: emission pass recomputes the blocks (MJG_OPT_REENCODE=1)
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
@@ -281,9 +280,9 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   const int npv = vt / 2 + 1;
   std::vector<int32_t> hcp((size_t)dw * (ht / 2)), vcp((size_t)dh * npv, 0), vps(dh);
   // D4 layout when every coefficient splits as 128 ch + cl, ch int8, cl in [-64, 64): per 4
-  // taps one word of ch bytes and one of cl bytes (MJG_SCALE_NO_D4=1: the pair layout)
+  // taps one word of ch bytes and one of cl bytes (else the int16 pair layout)
   std::vector<int32_t> hsum(dw, 0);
-  p.d4 = getenv("MJG_SCALE_NO_D4") == nullptr;
+  p.d4 = true;
   for (size_t i = 0; i < p.hf.coeff.size(); i++)
     if (p.hf.coeff[i] < -128 * 128 - 64 || p.hf.coeff[i] >= 127 * 128 + 64) p.d4 = false;
   for (int x = 0; x < dw; x++) {
@@ -369,9 +368,6 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
        (rc = dmalloc(&S.d_symn, B * NC * 64))))
     return rc;
   if (g.debug_coefs && (rc = dmalloc(&S.d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
-#ifdef MJG_STAMPS
-  if (!S.d_dbg && (rc = dmalloc(&S.d_dbg, (size_t)1 << 22))) return rc;  // 512K stamps
-#endif
   HIP_TRY(hipHostMalloc((void **)&S.h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void **)&S.h_status, 16, hipHostMallocDefault));
   HIP_TRY(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
@@ -453,7 +449,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
                         c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
-  c->reencode = getenv("MJG_OPT_REENCODE") != nullptr;
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
@@ -568,8 +563,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
-  if (const char *e = getenv("MJG_ENC_WG_PER_CU")) per_cu = atoi(e);  // perf experiments
-  if (getenv("MJG_DEBUG_GRID")) fprintf(stderr, "mjg: %d CUs, %d k_encode workgroups per CU\n", ncu, per_cu);
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
   {
     const int rc2 = dmalloc(&c->d_stage_bits, (size_t)c->enc_grid * kWavesPerWg * 64 * kStageWords);
@@ -620,11 +613,11 @@ void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntas
   if (g.range_convert)
     k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        S.d_ftabs, c->d_stage_bits, S.d_syms, S.d_symn);
+        c->d_stage_bits, S.d_syms, S.d_symn);
   else
     k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        S.d_ftabs, c->d_stage_bits, S.d_syms, S.d_symn);
+        c->d_stage_bits, S.d_syms, S.d_symn);
 }
 
 }  // namespace
@@ -752,9 +745,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     HIP_TRY(hipGetLastError());
   }
   tmark(c, S, MJG_K_ENCODE, 0);
-  if (c->optimal && c->reencode)  // MJG_OPT_REENCODE=1: recompute the blocks (A/B)
-    launch_encode<kEmitFrame>(c, S, enc_in, wgs, ntasks);
-  else if (c->optimal)
+  if (c->optimal)
     k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, c->stream>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
                                                                   S.d_scratch, S.d_chunk_bits, c->d_stage_bits,
                                                                   ntasks);
@@ -988,11 +979,3 @@ int mjg_debug_filter(mjg_ctx *c, int plane, int dir, int16_t *coeff, int32_t *po
 
 }  // extern "C"
 
-#ifdef MJG_STAMPS
-extern "C" int mjg_debug_stamps(mjg_ctx *c, uint64_t *out, size_t n) {
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipStreamSynchronize(c->tail));
-  HIP_TRY(hipMemcpy(out, c->slot[0].d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  return MJG_OK;
-}
-#endif

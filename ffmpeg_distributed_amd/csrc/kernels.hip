@@ -21,27 +21,9 @@
 
 #include "jpeg_tables.h"
 
-#ifndef MJG_ENC_WAVES_PER_EU
-#define MJG_ENC_WAVES_PER_EU 3  // k_encode occupancy target (waves per SIMD); measured best (v8)
-#endif
-#ifndef MJG_TEMPORAL_LOADS
-#define MJG_TEMPORAL_LOADS 1  // 1: plain (L2-retained) pixel row loads; 0: nontemporal (reads 1.64x the input, same time)
-#endif
-#ifndef MJG_RC_LUT
-#define MJG_RC_LUT 1  // tv->pc range conversion through a 512-byte LDS table (0: fp32 fma + med3)
-#endif
-#ifndef MJG_ROW_DOT2
-#define MJG_ROW_DOT2 0  // 1: row pass on packed int16 butterflies + v_dot2_i32_i16 (measured no faster: v_mov
-                        // for each biased accumulator, v_perm to pair the LDS table reads)
-#endif
-#ifndef MJG_ABLATE
-#define MJG_ABLATE 0  // perf experiments only: 1 no entropy coding, 2 +no column pass, 3 +no row pass, 4 no window pack/store,
-                      // 5 candidates not quantised exactly (v = 1 or 2), 6 no zigzag scatter of the
-                      // candidate bits, 7 no long-block (> 128 bits) re-emission, 8 at most 12
-                      // candidates per block
-#endif
-
 namespace mjg {
+
+constexpr int kEncWavesPerEU = 3;  // k_encode occupancy target (waves per SIMD); measured best (v8)
 
 constexpr int kMaxBlockBits = 1664;  // >= DC 16 + 63 * (16 + 10) bits
 constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 blocks
@@ -327,12 +309,8 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
     const bool two = cand != 0;
     const int k2 = two ? (int)__builtin_ctzll(cand) : k1;
     cand &= cand - 1;  // no-op when cand == 0
-#if MJG_ABLATE == 5
-    const int v1 = 1 + (k1 & 1), v2 = 1 + (k2 & 1);
-#else
     const int v1 = exact_coef(pkcol, zz[k1], m2, qc);
     const int v2 = exact_coef(pkcol, zz[k2], m2, qc);
-#endif
     emit_ac(k1, v1, prev, sink);
     if (two) emit_ac(k2, v2, prev, sink);
   }
@@ -378,13 +356,10 @@ __device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s) {
   const bool fast = (s.x0 + 8 <= s.pw) && (s.y0 + 8 <= s.ph) &&
                     ((((uintptr_t)base) | (uintptr_t)s.stride) & 7) == 0;
   if (fast) {
+    // plain loads: a chunk's row segments straddle 64-B sectors shared with the
+    // neighbouring chunk, which L2 keeps for its wave (nontemporal loads read 1.64x)
 #pragma unroll
-    for (int r = 0; r < 8; r++)
-#if MJG_TEMPORAL_LOADS
-      raw[r] = *(const uint64_t *)(base + (size_t)r * s.stride);
-#else
-      raw[r] = __builtin_nontemporal_load((const uint64_t *)(base + (size_t)r * s.stride));
-#endif
+    for (int r = 0; r < 8; r++) raw[r] = *(const uint64_t *)(base + (size_t)r * s.stride);
   }
   return fast;
 }
@@ -453,13 +428,7 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
-#ifndef MJG_GRP_SCAN
-#define MJG_GRP_SCAN 1  // pack_chunk group ORs by prefix sum + one bpermute (0: 4-step shuffle OR)
-#endif
-#ifndef MJG_ENC_BATCH
-#define MJG_ENC_BATCH 16
-#endif
-constexpr int kBatch = MJG_ENC_BATCH;  // chunks per work unit pulled from the counter
+constexpr int kBatch = 16;  // chunks per work unit pulled from the counter (8 ties, 32 is 5% slower)
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
 // quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
@@ -496,9 +465,9 @@ __device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, boo
 }
 
 // MODE: kEmitDefault (-huffman default, Annex K tables), kCount (-huffman optimal pass 1:
-// per-frame symbol histograms into hist[frame][544]), kEmitFrame (-huffman optimal pass 2:
-// the frame's own tables from ftabs[frame][544], built by k_huff_build).
-constexpr int kEmitDefault = 0, kCount = 1, kEmitFrame = 2;
+// per-frame symbol histograms into hist[frame][544] and each block's symbol records, which
+// k_emit_syms replays with the frame's own tables).
+constexpr int kEmitDefault = 0, kCount = 1;
 constexpr int kFrameTabWords = 544;  // AC luma, AC chroma, DC luma, DC chroma (table block layout)
 
 // Pack a chunk's 64 block codes into its slot: a wave prefix-scan of the block lengths gives
@@ -518,8 +487,8 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
   const uint32_t sft = off & 31, fw = off >> 5;
   const uint32_t lw = has ? (off + q.bits - 1) >> 5 : fw;
   uint32_t head = 0, tail = 0;
-  if (has && MJG_ABLATE != 4) {
-    if (q.bits <= 128 || MJG_ABLATE == 7) {
+  if (has) {
+    if (q.bits <= 128) {
       // the block's words from its end: d[4] = word lw, d[4 - j] = word lw - j, i.e. the
       // right-aligned 128 bits shifted left by t, the free bits after the block in word lw
       const uint32_t t = (32u - ((off + q.bits) & 31u)) & 31u, sh = 32u - t;  // sh in 1..32
@@ -554,7 +523,6 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
       }
     }
   }
-#if MJG_GRP_SCAN
   // Group OR of the heads of the lanes that start inside word fw, needed at the group's
   // first lane.  Heads of one word occupy disjoint bits, so their OR is their sum: with H
   // the inclusive prefix sum of the heads (mod 2^32), the group's OR is H[last] - H[first]
@@ -566,21 +534,10 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
   const int last = later ? lane + (int)__builtin_ctzll(later) : 63;
   const uint32_t H = wave_incl_scan(head, lane);
   const uint32_t grp = (uint32_t)__builtin_amdgcn_ds_bpermute(last << 2, (int)H) - H + head;  // valid at group firsts
-#else
-  // Every active block is at least 2 bits (a DC code and an EOB or coefficient-63 code,
-  // each >= 1 bit), so at most 16 active lanes start inside one word: distances 1..15
-  // (steps 1, 2, 4, 8) reach the whole group.  Inactive lanes (the chunk's tail) add 0.
-  uint32_t grp = head;
-#pragma unroll
-  for (int d = 1; d < 16; d <<= 1) {
-    const uint32_t v = __shfl_down(grp, d, 64), f = __shfl_down(fw, d, 64);
-    if (lane + d < 64 && f == fw) grp |= v;
-  }
-#endif
   // lane + 1's values (DPP wave_shl:1; lane 63 reads the old 0 / ~0u)
   const uint32_t gnext = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)grp, 0x130, 0xf, 0xf, false);
   const uint32_t fnext = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)fw, 0x130, 0xf, 0xf, false);
-  if (has && MJG_ABLATE != 4) {
+  if (has) {
     if (lw > fw) slot[lw] = tail | ((lane < 63 && fnext == lw) ? gnext : 0u);
     if (sft == 0) slot[fw] = grp;  // word-aligned start: this lane opens word fw
   }
@@ -588,11 +545,11 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
 }
 
 template <bool RC, int MODE>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
-__global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_encode(
+__global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
-    uint32_t *__restrict__ hist, const uint32_t *__restrict__ ftabs, uint32_t *__restrict__ stage_all,
+    uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all,
     uint32_t *__restrict__ syms, uint32_t *__restrict__ symn) {
   __shared__ uint32_t s_ac[512];
   __shared__ uint32_t s_dc[32];
@@ -601,11 +558,11 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
   __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
-  __shared__ uint8_t s_rc[(MJG_RC_LUT || MJG_ROW_DOT2) ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
+  __shared__ uint8_t s_rc[RC ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
   __shared__ uint32_t s_skip[12];                  // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
-  // per wave: the current frame's histogram (kCount) or code tables (kEmitFrame)
+  // per wave: the current frame's histogram (kCount)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -623,7 +580,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     s_desc[tid] = tabs[672 + tid];
   }
   if (tid < 12) s_skip[tid] = tabs[680 + tid];
-  if ((MJG_RC_LUT || MJG_ROW_DOT2) && RC)
+  if (RC)
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
   uint32_t *s_pk = s_pk_all[wave];
@@ -636,21 +593,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
   const int nwaves = gridDim.x * kWavesPerWg;
   const int gw = blockIdx.x * kWavesPerWg + wave;
   const int nbatch = (ntasks + kBatch - 1) / kBatch;
-#ifdef MJG_STAMPS  // diagnostic build: per-wave start/end shader clock into dbg_coefs
-  const uint64_t stamp0 = __builtin_amdgcn_s_memtime();
-  struct StampOnExit {
-    uint64_t t0;
-    uint64_t *dst;
-    int lane;
-    __device__ ~StampOnExit() {
-      const uint64_t t1 = __builtin_amdgcn_s_memtime();
-      if (lane == 0) {
-        dst[0] = t0;
-        dst[1] = t1;
-      }
-    }
-  } stamp_guard{stamp0, (uint64_t *)dbg_coefs + 2 * gw, lane};
-#endif
   if (gw >= nbatch) return;
   const int nblk = g.seg_blocks;  // blocks of one entropy-coded segment
   constexpr bool rc = RC;
@@ -679,74 +621,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
     // (M' = 1.5*2^23 + 32768), which also leaves x + 32768 in the low 16 mantissa bits:
     // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
-    // [RC] swscale tv->pc per pixel: fma + round-to-integer via + M (M = 1.5*2^23) + clamp
-    // with med3 reproduces clip_u8((p * A21 - B21) >> 21) for all 256 p (checked
-    // exhaustively in tests/test_oracle.py); values then carry the +M bias, which the
-    // butterfly's differences cancel and its sums remove with one -2M.
-    const float rA = tab ? 0x1.237p+0f : 0x1.2a14p+0f;        // 2387456 / 2^21, 2441856 / 2^21
-    const float rB = tab ? -0x1.1b821p+4f : -0x1.29fbe8p+4f;  // -17.719253..., -18.624000...
-#if MJG_ABLATE == 3
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) s_pk[(r * 4 + j) * 64 + lane] = (uint32_t)(raw[r] >> (16 * (j & 1)));
-    if (false)
-#endif
-#if MJG_ROW_DOT2
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      // Row pass (jfdctint pass 1) on packed int16 pairs, exactly: pixel pairs A = (p0, p1),
-      // B = (p7, p6), C = (p3, p2), D = (p4, p5) -- v_perm of the row bytes, or [RC] two LDS
-      // table reads into the halves of one register (swscale's tv->pc value per pixel, the
-      // address (tab << 8) | pixel built by one v_perm) -- then the butterfly sums and
-      // differences two at a time (v_pk_add/sub_u16; every value fits int16), and each
-      // output as one or two v_dot2_i32_i16 of (t7, t6), (t4, t5), (t13, t12) or (t10, t11)
-      // with the LLM constants multiplied out (the kPass2Dot rows).  The accumulator starts
-      // at DESCALE's 256 plus 32768 << 9, so the shift by 9 leaves value + 32768, the u16
-      // the row image stores; rows 0 / 4 (x16, no descale) start at 32768.
-      const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
-      u16x2 A, B, C, D;
-      if (rc) {
-        const uint8_t *lut = s_rc;
-        const uint32_t t8 = (uint32_t)tab;
-        A.x = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0400u)];
-        A.y = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0401u)];
-        B.x = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0403u)];
-        B.y = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0402u)];
-        C.x = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0403u)];
-        C.y = lut[__builtin_amdgcn_perm(t8, lo, 0x0c0c0402u)];
-        D.x = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0400u)];
-        D.y = lut[__builtin_amdgcn_perm(t8, hi, 0x0c0c0401u)];
-      } else {
-        A = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u));
-        B = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c060c07u));
-        C = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c020c03u));
-        D = as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0c050c04u));
-      }
-      const u16x2 s01 = A + B, d76 = A - B, s32 = C + D, d45 = C - D;  // (t0,t1) (t7,t6) (t3,t2) (t4,t5)
-      const short2_t e = __builtin_bit_cast(short2_t, s01 + s32);      // (t10, t11)
-      const short2_t f = __builtin_bit_cast(short2_t, s01 - s32);      // (t13, t12)
-      const short2_t o76 = __builtin_bit_cast(short2_t, d76), o45 = __builtin_bit_cast(short2_t, d45);
-      constexpr int kB = 256 + (32768 << 9);
-#define MJG_C2(a, b) (short2_t{(short)(a), (short)(b)})
-#define MJG_D2(x, c, acc) __builtin_amdgcn_sdot2((x), MJG_C2 c, (acc), false)
-      const uint32_t o0 = (uint32_t)MJG_D2(e, (16, 16), 32768);
-      const uint32_t o4 = (uint32_t)MJG_D2(e, (16, -16), 32768);
-      const uint32_t o2 = (uint32_t)MJG_D2(f, (10703, 4433), kB) >> 9;
-      const uint32_t o6 = (uint32_t)MJG_D2(f, (4433, -10704), kB) >> 9;
-      const uint32_t o1 = (uint32_t)MJG_D2(o76, (11363, 9633), MJG_D2(o45, (2260, 6437), kB)) >> 9;
-      const uint32_t o3 = (uint32_t)MJG_D2(o76, (9633, -2259), MJG_D2(o45, (-6436, -11362), kB)) >> 9;
-      const uint32_t o5 = (uint32_t)MJG_D2(o76, (6437, -11362), MJG_D2(o45, (9633, 2261), kB)) >> 9;
-      const uint32_t o7 = (uint32_t)MJG_D2(o76, (2260, -6436), MJG_D2(o45, (-11363, 9633), kB)) >> 9;
-#undef MJG_D2
-#undef MJG_C2
-      s_pk[(r * 4 + 0) * 64 + lane] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);
-      s_pk[(r * 4 + 1) * 64 + lane] = __builtin_amdgcn_perm(o3, o2, 0x05040100u);
-      s_pk[(r * 4 + 2) * 64 + lane] = __builtin_amdgcn_perm(o5, o4, 0x05040100u);
-      s_pk[(r * 4 + 3) * 64 + lane] = __builtin_amdgcn_perm(o7, o6, 0x05040100u);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#else
+    // [RC] swscale tv->pc per pixel from a 512-byte LDS table (clip_u8((p * A21 - B21) >> 21),
+    // checked exhaustively in tests/test_oracle.py), OR'ed into the mantissa of M = 1.5*2^23:
+    // values then carry the +M bias, which the butterfly's differences cancel and its sums
+    // remove with one -2M.
 #pragma unroll
     for (int r = 0; r < 8; r++) {
       const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
@@ -760,23 +638,15 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       p[6] = (float)((hi >> 16) & 255u);  // v_cvt_f32_ubyte2
       p[7] = (float)((hi >> 24) & 255u);  // v_cvt_f32_ubyte3
       float t0, t1, t2, t3;
-      if (rc && MJG_RC_LUT) {
+      if (rc) {
         // LDS address (tab << 8) | pixel in one v_perm, the table byte OR'ed into kM's
-        // mantissa: kM + range(p) exactly as the fp32 path below produces it
+        // mantissa: the fp32 value kM + range(p)
 #pragma unroll
         for (int x = 0; x < 8; x++) {
           const uint32_t a = __builtin_amdgcn_perm((uint32_t)tab, x < 4 ? lo : hi,
                                                    0x0c0c0400u | (uint32_t)(x & 3));
           p[x] = __uint_as_float(0x4B400000u | (uint32_t)s_rc[a]);
         }
-        t0 = (p[0] - 2.0f * kM) + p[7];
-        t1 = (p[1] - 2.0f * kM) + p[6];
-        t2 = (p[2] - 2.0f * kM) + p[5];
-        t3 = (p[3] - 2.0f * kM) + p[4];
-      } else if (rc) {
-#pragma unroll
-        for (int x = 0; x < 8; x++)
-          p[x] = __builtin_amdgcn_fmed3f(__builtin_fmaf(p[x], rA, rB) + kM, kM, kM + 255.0f);
         t0 = (p[0] - 2.0f * kM) + p[7];
         t1 = (p[1] - 2.0f * kM) + p[6];
         t2 = (p[2] - 2.0f * kM) + p[5];
@@ -808,7 +678,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
             __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
       __builtin_amdgcn_sched_barrier(0);
     }
-#endif
     // prefetch the next chunk while this one is encoded
     const int cur_frame = frame, cur_chunk = chunk, cur_bbase = bbase;
     const bool cur_active = active;
@@ -836,11 +705,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
     int dc = 0;
     uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
-#if MJG_ABLATE >= 2 && MJG_ABLATE <= 3
-    ca = s_pk[lane] & 0x10101010u;
-    cb = s_pk[64 + lane] & 0x1010u;
-    if (false)
-#endif
     if (cur_active) {
 #pragma unroll
       for (int jp = 0; jp < 4; jp++) {
@@ -931,10 +795,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     }
     // candidate bits -> zigzag-ordered mask (a handful of candidates per block)
     uint64_t mask = 0;
-#if MJG_ABLATE == 6
-    mask = ((uint64_t)cb << 32) | (ca << 1);
-    ca = cb = 0;
-#endif
     while (ca) {
       const int pos = __builtin_ctz(ca);
       ca &= ca - 1;
@@ -946,9 +806,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       mask |= 1ull << s_scat[32 + pos];
     }
 
-#if MJG_ABLATE == 8  // perf experiment: heavy blocks cut to their first 12 candidates
-    for (int i = __popcll(mask); i > 12; i--) mask &= ~(1ull << (63 - __clzll(mask)));
-#endif
     // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.
     const int delta = desc_delta(dsc);
@@ -961,19 +818,14 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
     const int diff = dc - pred;
     carry = dc;
 
-    if (MODE != kEmitDefault && cur_frame != aux_frame) {
+    if (MODE == kCount && cur_frame != aux_frame) {  // flush the previous frame's counts
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS traffic is done
-      if (MODE == kCount) {  // flush the previous frame's counts
-        if (aux_frame >= 0)
-          for (int i = lane; i < kFrameTabWords; i += 64) {
-            const uint32_t v = s_aux[i];
-            if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
-            s_aux[i] = 0;
-          }
-      } else {
-        for (int i = lane; i < kFrameTabWords; i += 64)
-          s_aux[i] = ftabs[(size_t)cur_frame * kFrameTabWords + i];
-      }
+      if (aux_frame >= 0)
+        for (int i = lane; i < kFrameTabWords; i += 64) {
+          const uint32_t v = s_aux[i];
+          if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
+          s_aux[i] = 0;
+        }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       aux_frame = cur_frame;
     }
@@ -990,23 +842,14 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MJG_ENC_WAVES_PER_EU) void k_enco
       t = tn;
       continue;
     }
-    const uint32_t *act = MODE == kEmitFrame ? s_aux + tab * 256 : s_ac + tab * 256;
-    const uint32_t *dct = MODE == kEmitFrame ? s_aux + 512 + tab * 16 : s_dc + tab * 16;
     ShiftSink q;
-    q.act = act;
-    q.dct = dct;
+    q.act = s_ac + tab * 256;
+    q.dct = s_dc + tab * 16;
     q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
-#if MJG_ABLATE == 0 || MJG_ABLATE >= 4
     if (cur_active) {
       emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
       if (q.bits > 128) q.flush();
     }
-#else
-    if (cur_active) {
-      q.emit((uint32_t)mask & 0xffffu, 16);
-      q.finish();
-    }
-#endif
     pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     if (tn < 0) break;
     if (new_batch) {

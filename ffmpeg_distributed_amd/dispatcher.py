@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import hashlib
+import json
 import os
 import queue
 import re
@@ -73,11 +74,44 @@ class Task:
     ffmpeg_args: List[str] = field(default_factory=list)
 
 
+class _LineFeed:
+    """Lines of a text pipe (universal newlines: ffmpeg ends progress lines with \\r),
+    read by a daemon thread into a queue so the follower can wait with a timeout and
+    notice stop() promptly, as the reference's select.poll loop does (fd.py:61-68)."""
+
+    _EOF = object()
+
+    def __init__(self, pipe):
+        self.q: "queue.Queue" = queue.Queue()
+        self.eof = False
+        threading.Thread(target=self._pump, args=(pipe,), daemon=True).start()
+
+    def _pump(self, pipe):
+        try:
+            for line in pipe:
+                self.q.put(line)
+        except (OSError, ValueError):
+            pass
+        self.q.put(self._EOF)
+
+    def get(self, timeout: float):
+        """The next line, None on timeout; sets .eof (and returns None) at end of stream."""
+        try:
+            item = self.q.get(timeout=timeout)
+        except queue.Empty:
+            return None
+        if item is self._EOF:
+            self.eof = True
+            return None
+        return item
+
+
 class FFMPEGProc:
     """Runs one command with stdin/stdout redirected, follows its stderr: progress lines
     go to `update_callback(frame, fps, time_s, duration_s, speed)`, every other line is
     kept in `.stderr` (reported if the command fails).  stop() only stops following
-    (the reference never kills the child either, fd.py:56-57)."""
+    (the reference never kills the child either, fd.py:56-57); it takes effect within
+    0.1 s even while the child writes nothing (fd.py:61-68 polls stderr with a timeout)."""
 
     def __init__(self, cmd, shell=False, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL,
                  update_callback: Optional[Callable] = None, env=None):
@@ -95,28 +129,41 @@ class FFMPEGProc:
     def stop(self):
         self._stop.set()
 
+    def _line(self, line: str):
+        prog = parse_progress(line)
+        if prog is None:
+            self.stderr += line
+            if self.duration is None:
+                self.duration = parse_duration(line)
+        elif self.update_callback:
+            frame, fps, t, speed = prog
+            self.update_callback(frame, fps, t, self.duration, speed)
+
     def run(self) -> int:
         self.proc = subprocess.Popen(self.cmd, shell=self.shell, stdin=self.stdin, stdout=self.stdout,
                                      stderr=subprocess.PIPE, universal_newlines=True, env=self.env)
-        for line in self.proc.stderr:
-            if self._stop.is_set():
+        feed = _LineFeed(self.proc.stderr)
+        while not self._stop.is_set():
+            line = feed.get(0.1)
+            if line is not None:
+                self._line(line)
+            elif feed.eof:
                 break
-            prog = parse_progress(line)
-            if prog is None:
-                self.stderr += line
-                if self.duration is None:
-                    self.duration = parse_duration(line)
-            elif self.update_callback:
-                frame, fps, t, speed = prog
-                self.update_callback(frame, fps, t, self.duration, speed)
         # stderr can reach EOF a moment before the child exits: the reference's loop runs
         # until poll() sees the exit (fd.py:62), so wait for it unless stop() was called
         # (then, like fd.py:85-89, give it one second and report whatever is there)
+        if not self._stop.is_set():
+            self.proc.wait()
+            return self.proc.returncode
         try:
-            rest = self.proc.communicate(timeout=None if not self._stop.is_set() else 1)[1]
-            self.stderr += rest or ""
+            self.proc.wait(timeout=1)
         except subprocess.TimeoutExpired:
             pass
+        while True:
+            line = feed.get(0)
+            if line is None:
+                break
+            self.stderr += line
         return self.proc.returncode
 
 
@@ -159,16 +206,24 @@ def server_argv(host: str, ffmpeg_args: List[str]) -> List[str]:
 SERVE_DONE = "mjg-serve: segment done rc="
 
 
+def serve_request(input_file: str, output_file: str) -> str:
+    """One worker.serve request line: the two absolute paths as a JSON array, so any path
+    (tabs, newlines, quotes) survives the one-line-per-segment protocol."""
+    return json.dumps([os.path.abspath(input_file), os.path.abspath(output_file)]) + "\n"
+
+
 class GpuServer:
     """One long-lived `worker --serve` process per gpu:N TaskThread.  run_task hands it one
     segment (a request line with the input and output paths) and follows its stderr like
     FFMPEGProc follows a per-segment worker, up to the segment's done line; its exit code is
     the segment's.  A server that dies fails the segment (re-queued by the caller, as for a
-    failed per-segment worker) and is started again for the next one."""
+    failed per-segment worker) and is started again for the next one.  A stop event set
+    while a segment runs closes the server and fails the segment."""
 
     def __init__(self, host: str):
         self.host = host
         self.proc: Optional[subprocess.Popen] = None
+        self.feed: Optional[_LineFeed] = None
         self.args: Optional[List[str]] = None
         self.stderr = ""
         self.duration: Optional[float] = None
@@ -179,19 +234,30 @@ class GpuServer:
         self.proc = subprocess.Popen(server_argv(self.host, ffmpeg_args), stdin=subprocess.PIPE,
                                      stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                                      universal_newlines=True, bufsize=1)
+        self.feed = _LineFeed(self.proc.stderr)
 
-    def run_task(self, task: "Task", update_callback: Optional[Callable] = None) -> int:
+    def run_task(self, task: "Task", update_callback: Optional[Callable] = None,
+                 stop: Optional[threading.Event] = None) -> int:
         if self.proc is None or self.proc.poll() is not None or self.args != list(task.ffmpeg_args):
             self._start(task.ffmpeg_args)
         self.stderr, self.duration = "", None
         try:
-            self.proc.stdin.write(f"{os.path.abspath(task.input_file)}\t{os.path.abspath(task.output_file)}\n")
+            self.proc.stdin.write(serve_request(task.input_file, task.output_file))
             self.proc.stdin.flush()
         except (BrokenPipeError, OSError):
             self.stderr = f"{self.host}: worker server is gone\n"
             self.close()
             return 1
-        for line in self.proc.stderr:
+        while True:
+            if stop is not None and stop.is_set():
+                self.stderr += f"{self.host}: stopped\n"
+                self.close(kill=True)
+                return 1
+            line = self.feed.get(0.1)
+            if line is None:
+                if self.feed.eof:
+                    break
+                continue
             if line.startswith(SERVE_DONE):
                 return int(line[len(SERVE_DONE):].strip() or 1)
             prog = parse_progress(line)
@@ -207,12 +273,14 @@ class GpuServer:
         self.proc = None
         return rc or 1
 
-    def close(self):
+    def close(self, kill: bool = False):
         if self.proc is not None:
             try:
                 self.proc.stdin.close()
             except OSError:
                 pass
+            if kill and self.proc.poll() is None:
+                self.proc.kill()
             self.proc.wait()
             self.proc = None
 
@@ -253,7 +321,7 @@ class TaskThread(threading.Thread):
                 break
             self.current = os.path.basename(task.input_file)
             if self.server is not None:
-                rc = self.server.run_task(task, self._progress)
+                rc = self.server.run_task(task, self._progress, self._stop_evt)
                 err = self.server.stderr
             else:
                 with open(task.input_file, "rb") as src, open(task.output_file, "wb") as dst:

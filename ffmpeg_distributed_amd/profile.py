@@ -73,6 +73,30 @@ def _parse_scale(vf: str) -> Tuple[Tuple[int, int], Tuple[str, ...]]:
     return (W, H), flags
 
 
+def _flag_ops(v: str) -> List[Tuple[str, str]]:
+    """An AVOption flags string (`+a-b`, `a+b`, `a`) as (op, name) pairs; op '' replaces the
+    whole set (libavutil opt.c set_string_flags: a leading name without +/- starts from 0)."""
+    out, op, name = [], "", ""
+    for ch in v:
+        if ch in "+-":
+            if name:
+                out.append((op, name))
+            op, name = ch, ""
+        else:
+            name += ch
+    if name:
+        out.append((op, name))
+    if not out:
+        raise Unsupported(f"flags {v!r}")
+    return out
+
+
+def _apply_flag(cur: bool, ops: List[Tuple[str, str]]) -> bool:
+    for op, _ in ops:
+        cur = op != "-"
+    return cur
+
+
 def parse(args: Union[str, Sequence[str]]) -> Profile:
     """Profile for `remote_args`, or raise Unsupported(reason)."""
     a: List[str] = shlex.split(args) if isinstance(args, str) else list(args)
@@ -108,12 +132,20 @@ def parse(args: Union[str, Sequence[str]]) -> Profile:
             huff = val()
         elif o == "-bitexact":
             bitexact = True
-        elif o in ("-flags", "-flags:v", "-fflags"):
+        elif o in ("-flags", "-flags:v"):
+            # AVCodecContext.flags: the only codec flag on the GPU path is bitexact; any other
+            # (+gray, +qscale, ...) changes the bitstream, so it is not accepted silently
             v = val()
-            if "+bitexact" in v or v == "bitexact":
-                bitexact = True
-            else:
-                raise Unsupported(f"{o} {v}")
+            ops = _flag_ops(v)
+            if any(name != "bitexact" for _, name in ops):
+                raise Unsupported(f"{o} {v} (only bitexact is GPU-accelerated)")
+            bitexact = _apply_flag(bitexact, ops)
+        elif o == "-fflags":
+            # AVFormatContext.fflags: a muxer flag (format-level bitexact, no Lavf version
+            # strings); it never reaches the encoder, so it does not count as codec bitexact
+            v = val()
+            if any(name != "bitexact" for _, name in _flag_ops(v)):
+                raise Unsupported(f"-fflags {v}")
         elif o in ("-vf", "-filter:v"):
             scale, flags = _parse_scale(val())
         elif o in ("-an", "-sn", "-dn", "-y"):

@@ -91,3 +91,76 @@ def testsrc2_i420_torch(w: int, h: int, t0: int, n: int, device, full_range: boo
                   for c in range(3)]
         frames.append(torch.cat([p.to(torch.uint8).reshape(-1) for p in planes]))
     return torch.stack(frames)
+
+
+# ----------------------------------------------------------------- content sensitivity
+# Benchmark content beside testsrc2 (bench.py --content): the entropy coder's share of the
+# encode grows with the coded bits, so throughput depends on content.  Neither is a parity
+# input (the parity tests draw their own content); both are seeded and deterministic.
+
+def _fractal(torch, h, w, seed, device, octaves, amp0, decay):
+    """Value noise summed over octaves: a random grid of cell 2^k px, bicubic-upsampled,
+    amplitude amp0 * decay^(octave) -- a 1/f-like spectrum with natural-image statistics."""
+    import torch.nn.functional as F
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    acc = torch.zeros((1, 1, h, w), dtype=torch.float32, device=device)
+    amp = amp0
+    for cell in octaves:
+        gh, gw = h // cell + 3, w // cell + 3
+        grid = torch.randn((1, 1, gh, gw), generator=g, device=device)
+        up = F.interpolate(grid, size=(gh * cell, gw * cell), mode="bicubic", align_corners=False)
+        acc += amp * up[:, :, cell:cell + h, cell:cell + w]
+        amp *= decay
+    return acc[0, 0]
+
+
+def natural_i420_torch(w: int, h: int, t0: int, n: int, device, full_range: bool = False):
+    """n frames of fractal (1/f) value noise: smooth regions, textures and soft edges at every
+    scale, about the coded size of camera footage at q=5 (several times testsrc2's)."""
+    import torch
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    frames = []
+    scale = max(1, w // 480)
+    oct_y = [c * scale for c in (256, 128, 64, 32, 16, 8, 4)] + [2, 1]
+    oct_c = [c * scale for c in (128, 64, 32, 16, 8)]
+    for t in range(t0, t0 + n):
+        y = 118 + _fractal(torch, h, w, 1000 + t, device, oct_y, 38.0, 0.75)
+        u = 128 + _fractal(torch, ch, cw, 2000 + t, device, oct_c, 16.0, 0.7)
+        v = 128 + _fractal(torch, ch, cw, 3000 + t, device, oct_c, 16.0, 0.7)
+        lo, hi = (0, 255) if full_range else (16, 235)
+        planes = [y.clamp(lo, hi), u.clamp(lo, 240 if not full_range else 255),
+                  v.clamp(lo, 240 if not full_range else 255)]
+        frames.append(torch.cat([p.round().to(torch.uint8).reshape(-1) for p in planes]))
+    return torch.stack(frames)
+
+
+def noise_patches_i420_torch(w: int, h: int, t0: int, n: int, device, full_range: bool = False,
+                             frac: float = 0.125):
+    """testsrc2 frames with a seeded `frac` of their 16x16 macroblocks replaced by uniform
+    noise (Y and the co-sited 8x8 chroma): worst-case blocks (~40 nonzero coefficients,
+    long codes, 0xFF stuffing) scattered among cheap ones."""
+    import torch
+    base = testsrc2_i420_torch(w, h, t0, n, device, full_range)
+    mbw, mbh = w // 16, h // 16
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    g = torch.Generator(device=device)
+    for i in range(n):
+        g.manual_seed(7000 + t0 + i)
+        sel = (torch.rand((mbh, mbw), generator=g, device=device) < frac)
+        my = sel.repeat_interleave(16, 0).repeat_interleave(16, 1)
+        mc = sel.repeat_interleave(8, 0).repeat_interleave(8, 1)
+        f = base[i]
+        y = f[: w * h].view(h, w)
+        u = f[w * h: w * h + cw * ch].view(ch, cw)
+        v = f[w * h + cw * ch:].view(ch, cw)
+        for p, m in ((y, my), (u, mc), (v, mc)):
+            hh, ww = m.shape
+            noise = torch.randint(0, 256, (hh, ww), generator=g, device=device, dtype=torch.uint8)
+            sub = p[:hh, :ww]
+            sub[m] = noise[m]
+    return base
+
+
+CONTENT = {"testsrc": testsrc2_i420_torch, "natural": natural_i420_torch,
+           "noise-patches": noise_patches_i420_torch}

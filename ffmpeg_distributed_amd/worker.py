@@ -18,6 +18,7 @@ the GPU path: the decoded frames then go to the real ffmpeg as y4m (`ffmpeg_fall
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import queue
 import subprocess
@@ -189,19 +190,32 @@ class Source:
         except ValueError as e:
             raise ValueError(f"V_UNCOMPRESSED {e}") from None
         finally:
-            for f in futs:
-                f.result()
+            # every positional read has finished before the batch buffer is handed on (or
+            # freed on an error path), failed or not; then the first failure is raised
+            from concurrent.futures import wait
+            wait(futs)
+        for f in futs:
+            f.result()
         return got
 
-    def close(self) -> int:
+    def close(self, kill: bool = False) -> int:
+        """Stop reading: join the pread pool; close the decoder child's output and wait for
+        it (kill=True, on an error path: terminate it first).  Returns its exit code."""
         pool = getattr(self, "_pool", None)
         if pool is not None:
-            pool.shutdown()
+            pool.shutdown(wait=True)
             self._pool = None
         if self.child is None:
             return 0
-        self.child.stdout.close()
-        return self.child.wait()
+        if kill and self.child.poll() is None:
+            self.child.kill()
+        try:
+            self.child.stdout.close()
+        except OSError:
+            pass
+        rc = self.child.wait()
+        self.child = None
+        return rc
 
 
 def _fd_or_none(f):
@@ -299,6 +313,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     fb = enc.frame_bytes
     free: "queue.Queue[int]" = queue.Queue()
     full: "queue.Queue" = queue.Queue()
+    abort = threading.Event()
     for i in range(nbuf):
         free.put(i)
 
@@ -306,7 +321,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         try:
             while True:
                 i = free.get()
-                if i < 0:
+                if i < 0 or abort.is_set():
                     return
                 n = src.read_into(bufs[i].array, batch)
                 full.put((i, n))
@@ -332,6 +347,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         frames += m
         prog.update(frames, sum(len(p) for p in packets))
 
+    failed = True
     try:
         while True:
             item = full.get()
@@ -351,20 +367,29 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
             drain_one()
         mkv.close()
         prog.update(frames, 0, final=True)
-    except BaseException:
-        if cache is not None:  # a submit may still be queued: start the next segment afresh
-            cache.pop("key", None)
-            cache.pop("enc", None)
-            cache.pop("bufs", None)
-            cache = None
-        raise
+        failed = False
     finally:
+        # Nothing is freed while a reader could still write into a batch buffer: stop the
+        # reader thread (it finishes at most the read in flight, whose positional reads it
+        # waits for), killing a decoder child whose pipe it may be blocked on; then close
+        # the source, and only then the encoder and the page-locked buffers.
+        abort.set()
         free.put(-1)
+        th.join(timeout=5.0)
+        if th.is_alive():
+            src.close(kill=True)
+            th.join(timeout=5.0)
+        stuck = th.is_alive()  # blocked on a stdin pipe that never delivers: leak, never free
+        rc = src.close(kill=failed)
+        if (failed or stuck) and cache is not None:  # a submit may still be queued: start afresh
+            for k in ("key", "enc", "bufs"):
+                cache.pop(k, None)
+            cache = None
         if cache is None:
             enc.close()
-            for b in bufs:
-                b.free()
-    rc = src.close()
+            if not stuck:
+                for b in bufs:
+                    b.free()
     if rc:
         stderr.write(f"decoder exited with {rc}\n")
         return 1
@@ -388,7 +413,8 @@ def serve(device: int, args: List[str], requests=None, stderr=None) -> int:
     """Persistent worker (dispatcher --persistent-gpu-workers): one process per `-H gpu:N`
     entry encodes segment after segment, keeping its HIP context, encoder and page-locked
     buffers, so a segment no longer pays process start + HIP init + allocation (~0.5 s).
-    Each request line on stdin is `INPUT<TAB>OUTPUT`; the segment runs exactly as `run`
+    Each request line on stdin is a JSON array `[INPUT, OUTPUT]` (dispatcher.serve_request:
+    any path survives, tabs and newlines included); the segment runs exactly as `run`
     runs it for one process (same output bytes, same ffmpeg-style stderr lines), then
     `mjg-serve: segment done rc=N` on stderr ends it.  EOF on stdin ends the server."""
     requests = requests or sys.stdin
@@ -400,7 +426,7 @@ def serve(device: int, args: List[str], requests=None, stderr=None) -> int:
             if not line:
                 continue
             try:
-                src, dst = line.split("\t")
+                src, dst = json.loads(line)
                 with open(src, "rb") as fin, open(dst, "wb") as fout:
                     rc = run(device, args, stdin=fin, stdout=fout, stderr=stderr, cache=cache)
             except Exception as e:

@@ -227,8 +227,20 @@ def test_scale_matches_oracle(sw, sh, dw, dh, full):
     assert got == oracle_frames(frames, sw, sh, q, full, dw, dh)
 
 
+def _oracle_many(frames, w, h, **kw):
+    """The oracle over many frames on a thread pool (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(f):
+        y, u, v = split_i420(f, w, h)
+        return oracle.encode_frame(y, u, v, **kw)
+
+    with ThreadPoolExecutor(16) as ex:
+        return list(ex.map(one, frames))
+
+
 def test_4k_full_size_properties():
-    """BASELINE config 2 size: decodable, deterministic, equal to the oracle on frame 0."""
+    """BASELINE config 2 size: every frame equal to the oracle, decodable, deterministic."""
     from PIL import Image
     w, h = 3840, 2160
     frames = np.stack([make_testsrc(w, h, t) for t in range(4)])
@@ -240,8 +252,49 @@ def test_4k_full_size_properties():
         im = Image.open(io.BytesIO(j))
         im.load()
         assert im.size == (w, h)
-    y, u, v = split_i420(frames[0], w, h)
-    assert a[0] == oracle.encode_frame(y, u, v, qscale=5)
+    ref = _oracle_many(frames, w, h, qscale=5)
+    for i in range(4):
+        assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
+
+
+def test_4k_segment_batch_from_device_memory():
+    """The bench's exact submission: one 120-frame 4K segment (BASELINE configs[1], a 2 s
+    segment at 60 fps) generated in HBM and submitted by device pointer, two submits
+    queued; every frame of both submits byte-equal to the oracle."""
+    import torch
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    w, h, n = 3840, 2160, 120
+    dev = torch.device("cuda", 0)
+    pool = torch.empty((n, i420_frame_bytes(w, h)), dtype=torch.uint8, device=dev)
+    for i in range(0, n, 20):
+        pool[i:i + 20] = testsrc2_i420_torch(w, h, 1000 + i, 20, dev)
+    torch.cuda.synchronize()
+    host = pool.cpu().numpy()
+    assert (host[59] == make_testsrc(w, h, 1059)).all()  # the device generator = the host one
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=n) as enc:
+        enc.submit(device_ptr=pool.data_ptr(), nframes=n)
+        enc.submit(device_ptr=pool[60].data_ptr(), nframes=60)
+        s0 = enc.sync()
+        a = enc.fetch()
+        s1 = enc.sync()
+        b = enc.fetch()
+    ref = _oracle_many(host, w, h, qscale=5)
+    assert list(s0) == [len(r) for r in ref]
+    for i in range(n):
+        assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
+    assert list(s1) == [len(r) for r in ref[60:]] and b == ref[60:]
+
+
+def test_8k_yuvj420p_matches_oracle():
+    """BASELINE configs[4]: 7680x4320 yuvj420p q=5 (no range conversion), every frame of a
+    3-frame batch (and a ragged second submit) byte-equal to the oracle."""
+    w, h = 7680, 4320
+    frames = np.stack([make_testsrc(w, h, 40 + t, full_range=True) for t in range(3)])
+    with MjpegEncoder(0, w, h, qscale=5, full_range=True, max_batch=2) as enc:
+        got = enc.encode(frames)
+    ref = _oracle_many(frames, w, h, qscale=5, full_range=True)
+    for i in range(3):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
 # ------------------------------------------------ 4:2:2 / 4:4:4 and the RST layout (§8f row 4)
@@ -309,8 +362,8 @@ def test_scale_422_444_rst_matches_oracle(chroma, rst):
 
 
 def test_rst_4k_full_size():
-    """4K with RST (135 restart intervals per frame, 23 chunks per row): equal to the
-    oracle on frame 0, decodable, same pixels as the plain layout."""
+    """4K with RST (135 restart intervals per frame, 23 chunks per row): every frame equal
+    to the oracle, decodable, same pixels as the plain layout."""
     from PIL import Image
     w, h = 3840, 2160
     frames = np.stack([make_testsrc(w, h, t) for t in range(3)])
@@ -318,8 +371,9 @@ def test_rst_4k_full_size():
         a = enc.encode(frames)
     with MjpegEncoder(0, w, h, qscale=5, max_batch=3) as enc:
         b = enc.encode(frames)
-    y, u, v = split_i420(frames[0], w, h)
-    assert a[0] == oracle.encode_frame(y, u, v, qscale=5, rst=True)
+    ref = _oracle_many(frames, w, h, qscale=5, rst=True)
+    for i in range(3):
+        assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
     for ja, jb in zip(a, b):
         ia, ib = Image.open(io.BytesIO(ja)), Image.open(io.BytesIO(jb))
         assert np.array_equal(np.asarray(ia), np.asarray(ib))

@@ -2,6 +2,7 @@
 V_MJPEG Matroska segment out, every packet byte-identical to the CPU oracle's encode
 of the same frame (oracle/mjpeg_oracle.c restating ffmpeg's mjpeg/swscale path)."""
 import io
+import json
 from fractions import Fraction
 
 import numpy as np
@@ -134,7 +135,7 @@ def test_worker_serve_reuses_context_across_segments(tmp_path):
             wr.write_frame(f.tobytes())
         wr.close()
         (tmp_path / f"in{i}.mkv").write_bytes(buf.getvalue())
-        reqs.append(f"{tmp_path}/in{i}.mkv\t{tmp_path}/out{i}.mkv\n")
+        reqs.append(json.dumps([f"{tmp_path}/in{i}.mkv", f"{tmp_path}/out{i}.mkv"]) + "\n")
         want.append([oracle.encode_frame(*split_i420(f, w, h), full_range=False, qscale=q, sar=(1, 1))
                      for f in frames])
     err = io.StringIO()
@@ -143,3 +144,38 @@ def test_worker_serve_reuses_context_across_segments(tmp_path):
     for i in range(len(segs)):
         r = container.MkvReader(io.BytesIO((tmp_path / f"out{i}.mkv").read_bytes()))
         assert [d for _, d in r.frames(1)] == want[i], f"segment {i}"
+
+
+def _raw_mkv(frames, w, h):
+    buf = io.BytesIO()
+    wr = container.MkvWriter(buf, w, h, Fraction(25), codec="V_UNCOMPRESSED", colour_space=b"I420")
+    for f in frames:
+        wr.write_frame(f.tobytes())
+    wr.close()
+    return buf.getvalue()
+
+
+def test_worker_serve_segment_failing_mid_stream(tmp_path, monkeypatch):
+    """A segment that fails mid-stream (its file ends inside a frame after several batches
+    were submitted) reports rc 1; the reader thread and its positional reads are stopped
+    before the batch buffers are freed, and the next segments come out byte-exact."""
+    monkeypatch.setattr(worker, "BATCH", 2)
+    w, h, q = 96, 64, 5
+    good = [[make_testsrc(w, h, 5 * i + k) for k in range(7)] for i in range(3)]
+    bad = _raw_mkv([make_testsrc(w, h, 100 + k) for k in range(9)], w, h)
+    (tmp_path / "bad.mkv").write_bytes(bad[: len(bad) - w * h])  # last frame cut short
+    reqs = [json.dumps([str(tmp_path / "in0.mkv"), str(tmp_path / "out0.mkv")]),
+            json.dumps([str(tmp_path / "bad.mkv"), str(tmp_path / "outbad.mkv")]),
+            json.dumps([str(tmp_path / "in1.mkv"), str(tmp_path / "out1.mkv")]),
+            json.dumps([str(tmp_path / "in2.mkv"), str(tmp_path / "out2.mkv")])]
+    for i, frames in enumerate(good):
+        (tmp_path / f"in{i}.mkv").write_bytes(_raw_mkv(frames, w, h))
+    err = io.StringIO()
+    assert worker.serve(0, _args(q), requests=io.StringIO("\n".join(reqs) + "\n"), stderr=err) == 0
+    done = [l for l in err.getvalue().splitlines() if l.startswith(worker.SERVE_DONE)]
+    assert [int(l[len(worker.SERVE_DONE):]) for l in done] == [0, 1, 0, 0], err.getvalue()
+    assert "ends inside a frame" in err.getvalue()
+    for i, frames in enumerate(good):
+        r = container.MkvReader(io.BytesIO((tmp_path / f"out{i}.mkv").read_bytes()))
+        want = [oracle.encode_frame(*split_i420(f, w, h), full_range=False, qscale=q, sar=(1, 1)) for f in frames]
+        assert [d for _, d in r.frames(1)] == want, f"segment {i}"

@@ -41,14 +41,6 @@ def _int_array(name):
     return [int(eval(x)) for x in body.replace("\n", " ").split(",") if x.strip()]
 
 
-def _hexfloats():
-    s = _src()
-    a = re.search(r"const float rA = tab \? ([^ ]+) : ([^;]+);", s)
-    b = re.search(r"const float rB = tab \? ([^ ]+) : ([^;]+);", s)
-    f = lambda t: np.float32(float.fromhex(t.strip().rstrip("f")))
-    return {"C": (f(a.group(1)), f(b.group(1))), "Y": (f(a.group(2)), f(b.group(2)))}
-
-
 def fma32(a, b, c):
     """fp32 fused multiply-add: exact in float64 for these magnitudes, one rounding."""
     return (np.float64(np.float32(a)) * np.float64(np.float32(b)) + np.float64(np.float32(c))).astype(np.float32)
@@ -61,16 +53,23 @@ def range_int(p, chroma):
 
 
 def range_f32(p, chroma):
-    A, B = _hexfloats()["C" if chroma else "Y"]
-    r = (fma32(p.astype(np.float32), A, B) + M).astype(np.float32)
-    return np.minimum(np.maximum(r, M), (M + np.float32(255)).astype(np.float32))  # med3
+    """k_encode's [RC] pixel: the LDS table byte range(p) OR'ed into the mantissa of
+    M = 1.5 * 2^23, i.e. the fp32 value M + range(p)."""
+    byte = range_int(p, chroma).astype(np.uint32)
+    return (np.uint32(0x4B400000) | byte).view(np.float32)
 
 
 @pytest.mark.parametrize("chroma", [False, True])
-def test_fp32_range_convert_exhaustive(chroma):
+def test_range_lut_in_mantissa_exhaustive(chroma):
+    """The table (range_luma / range_chroma in kernels.hip) OR'ed into M's mantissa is the
+    fp32 value M + range(p) for all 256 inputs, and range() is swscale's tv->pc converter."""
     p = np.arange(256, dtype=np.int64)
     got = (range_f32(p, chroma).astype(np.float64) - float(M)).astype(np.int64)
     assert (got == range_int(p, chroma)).all()
+    src = _src()
+    a, b, sh = (596864, 9027848, 19) if chroma else (2441856, 38008785, 21)
+    assert f"__mul24(p, {a}) - {b}) >> {sh}" in src
+    assert (np.clip((p * a - b) >> sh, 0, 255) == range_int(p, chroma)).all()
 
 
 def pass1_int(p):

@@ -108,13 +108,13 @@ def test_dispatcher_spreads_segments_over_gpu_hosts(tmp_path, monkeypatch):
 
 
 STUB_SERVER = r"""
-import os, sys, time
+import json, os, sys, time
 dev = sys.argv[sys.argv.index("--device") + 1]
 assert sys.argv[-1] == "--serve"
 with open(os.environ["STUB_LOG"], "a") as log:
     log.write(f"start {dev}\n")
 for line in sys.stdin:
-    src, dst = line.rstrip("\n").split("\t")
+    src, dst = json.loads(line)
     data = open(src).read()
     time.sleep(0.05)
     if data.startswith("SEG2:") and not os.path.exists("crashed"):
@@ -173,6 +173,7 @@ def test_worker_serve_protocol(tmp_path, monkeypatch):
     """worker.serve: one request line per segment, the segment's files opened for run(),
     the done line carries run()'s exit code (an exception is a failed segment, rc 1)."""
     import io
+    import json
     from ffmpeg_distributed_amd import worker
     calls = []
 
@@ -189,7 +190,7 @@ def test_worker_serve_protocol(tmp_path, monkeypatch):
     reqs = []
     for i, body in enumerate([b"a", b"boom", b"rc7", b"b"]):
         (tmp_path / f"in{i}").write_bytes(body)
-        reqs.append(f"{tmp_path}/in{i}\t{tmp_path}/out{i}\n")
+        reqs.append(json.dumps([f"{tmp_path}/in{i}", f"{tmp_path}/out{i}"]) + "\n")
     err = io.StringIO()
     assert worker.serve(2, ["-q:v", "5"], requests=io.StringIO("".join(reqs)), stderr=err) == 0
     done = [l for l in err.getvalue().splitlines() if l.startswith(worker.SERVE_DONE)]
@@ -197,3 +198,68 @@ def test_worker_serve_protocol(tmp_path, monkeypatch):
     assert "ValueError: bad segment" in err.getvalue()
     assert (tmp_path / "out0").read_bytes() == b"out:a" and (tmp_path / "out3").read_bytes() == b"out:b"
     assert len({c[3] for c in calls}) == 1 and all(c[:2] == (2, ["-q:v", "5"]) for c in calls)
+
+
+def test_serve_request_survives_any_path(tmp_path, monkeypatch):
+    """Paths with tabs, newlines and quotes go through the one-line serve protocol intact."""
+    import io
+    from ffmpeg_distributed_amd import dispatcher as D, worker
+    seen = []
+
+    def fake_run(dev, args, stdin, stdout, stderr, cache):
+        seen.append(stdin.read())
+        stdout.write(b"ok")
+        return 0
+
+    monkeypatch.setattr(worker, "run", fake_run)
+    d = tmp_path / "a\tb\nc 'q\""
+    d.mkdir()
+    (d / "in.mkv").write_bytes(b"payload")
+    req = D.serve_request(str(d / "in.mkv"), str(d / "out.mkv"))
+    assert req.count("\n") == 1 and req.endswith("\n")
+    err = io.StringIO()
+    assert worker.serve(0, [], requests=io.StringIO(req), stderr=err) == 0
+    assert seen == [b"payload"] and (d / "out.mkv").read_bytes() == b"ok"
+    assert err.getvalue().strip().endswith(worker.SERVE_DONE + "0")
+
+
+def test_ffmpegproc_stop_is_prompt_while_child_is_silent():
+    """stop() ends the stderr follow loop within a poll period even when the child writes
+    nothing (fd.py:61-68 polls with a timeout); the child itself is not killed (fd.py:56-57)."""
+    import sys
+    import threading
+    from ffmpeg_distributed_amd import dispatcher as D
+    p = D.FFMPEGProc([sys.executable, "-c", "import time, sys; sys.stderr.write('hello\\n'); "
+                      "sys.stderr.flush(); time.sleep(30)"])
+    t = threading.Thread(target=p.run)
+    t0 = time.monotonic()
+    t.start()
+    time.sleep(0.5)
+    p.stop()
+    t.join(5)
+    try:
+        assert not t.is_alive()
+        assert time.monotonic() - t0 < 4
+        assert "hello" in p.stderr
+    finally:
+        p.proc.kill()
+        p.proc.wait()
+
+
+def test_gpu_server_stop_fails_the_running_segment(tmp_path):
+    """A stop event set while a persistent server works on a segment closes the server and
+    fails the segment instead of waiting for it."""
+    import sys
+    import threading
+    from ffmpeg_distributed_amd import dispatcher as D
+    stub = tmp_path / "silent.py"
+    stub.write_text("import sys, time\nfor line in sys.stdin:\n    time.sleep(60)\n")
+    srv = D.GpuServer("gpu:0")
+    srv._start = lambda args: (setattr(srv, "args", list(args)), setattr(srv, "proc", __import__("subprocess").Popen(
+        [sys.executable, str(stub)], stdin=-1, stdout=-3, stderr=-1, universal_newlines=True, bufsize=1)),
+        setattr(srv, "feed", D._LineFeed(srv.proc.stderr)))
+    stop = threading.Event()
+    threading.Timer(0.3, stop.set).start()
+    t0 = time.monotonic()
+    rc = srv.run_task(D.Task(str(tmp_path / "i"), str(tmp_path / "o"), []), stop=stop)
+    assert rc == 1 and time.monotonic() - t0 < 5 and srv.proc is None

@@ -80,10 +80,29 @@ def test_profile_qscale_mapping(q, expect):
     "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -pix_fmt gray",
     "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -thread_type auto",
     "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -slices many",
+    # -fflags is a muxer flag: it does not make the encoder bitexact (the Lavc COM remains)
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -fflags +bitexact",
+    # codec flags other than bitexact change the bitstream (+gray: flat chroma)
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -flags +gray+bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -flags +bitexact+qscale",
+    # bitexact switched off again
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -flags -bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact -fflags +genpts",
 ])
 def test_profile_rejects_outside_gpu_path(args):
     prof, why = profile.try_parse(args)
     assert prof is None and why
+
+
+@pytest.mark.parametrize("args", [
+    "-c:v mjpeg -q:v 5 -dct int -flags +bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -flags:v bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -bitexact -fflags +bitexact",
+    "-c:v mjpeg -q:v 5 -dct int -fflags +bitexact -flags +bitexact",
+])
+def test_profile_codec_bitexact_spellings(args):
+    prof, why = profile.try_parse(args)
+    assert prof is not None, why
 
 
 # ------------------------------------------------------------------ matroska

@@ -20,6 +20,19 @@ def load(dirs):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
+def load_totals(dirs):
+    """Per kernel: {counter: sum over all dispatches}, plus "dispatches"."""
+    acc = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for d in dirs:
+        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                name = r["Kernel_Name"].split("(")[0]
+                acc[name][r["Counter_Name"]] += float(r["Counter_Value"])
+                disp[name].add((f, r["Dispatch_Id"]))
+    return {k: dict(cs, dispatches=len(disp[k])) for k, cs in acc.items()}
+
+
 if __name__ == "__main__":
     res = load(sys.argv[1:])
     print(json.dumps(res, indent=1))

@@ -1,42 +1,81 @@
 #!/usr/bin/env python3
-"""Turn the tools/pmc_traffic.sh counter CSVs into profiles/pmc_encode_4k_q5.json:
-per-launch HBM bytes of k_encode = FETCH_SIZE x (calibrated bytes per unit) + WRITE_SIZE x 1024
-(WRITE_SIZE is exact for streaming stores per MI355X_MICROARCH.md; the chunk-slot stores
-are coalesced 4-byte-per-lane runs, noted as uncalibrated)."""
+"""Turn the tools/pmc_traffic.sh counter CSVs into profiles/pmc_<workload>.json: per kernel,
+HBM bytes per launch = FETCH_SIZE x (calibrated bytes per unit for the kernel's read width)
++ WRITE_SIZE x (calibrated bytes per unit for its write width).
+
+Calibration (tools/calib_fetch.hip) reads / writes a 1.5 GB buffer (past the 256 MiB L3)
+with 8 B, 4 B per lane loads and 4 B, 1 B per lane stores; each kernel is assigned the
+width of its dominant access (KERNEL_WIDTH).  Usage: pmc_traffic.py OUTDIR CAL_BYTES WL..."""
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_summary import load  # noqa: E402
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+from pmc_summary import load, load_totals  # noqa: E402
 
-out, calib_bytes = sys.argv[1], int(sys.argv[2])
-cal = load([os.path.join(out, "calib")])
-cal_fetch = sum(v["FETCH_SIZE"] for v in cal.values())  # one kernel
-per_unit = calib_bytes / cal_fetch
-def _enc(d):  # the k_encode instantiation (template arguments in the name)
-    return next(v for k, v in d.items() if "k_encode" in k)
-
-
-fetch = _enc(load([os.path.join(out, "fetch")]))["FETCH_SIZE"]
-write = _enc(load([os.path.join(out, "write")]))["WRITE_SIZE"]
-frames, W, H = 120, 3840, 2160
-res = {
-    "kernel": "mjg::k_encode",
-    "workload": {"frames_per_launch": frames, "width": W, "height": H, "qscale": 5,
-                 "input": "testsrc2-like yuv420p (tools/pmc_workload.py)"},
-    "calibration": {"kernel": "tools/calib_fetch.hip (8 B/lane coalesced reads)",
-                    "bytes": calib_bytes, "FETCH_SIZE": cal_fetch, "bytes_per_unit": per_unit},
-    "FETCH_SIZE": fetch, "WRITE_SIZE": write,
-    "read_bytes_per_launch": fetch * per_unit,
-    "write_bytes_per_launch": write * 1024,
-    "hbm_bytes_per_launch": fetch * per_unit + write * 1024,
-    "input_plane_bytes_per_launch": frames * W * H * 3 // 2,
+# dominant (read, write) access width of each kernel, bytes per lane
+KERNEL_WIDTH = {
+    "k_encode": (8, 4),       # 8-byte pixel row loads, slot words
+    "k_fused": (4, 4),        # 4-byte window loads (scale + encode), slot words
+    "k_scale": (4, 1),        # dword window loads, one output byte per lane
+    "k_emit_syms": (4, 4),    # symbol record words, slot words
+    "k_count_ff": (4, 4),     # slot words
+    "k_write": (4, 1),        # slot words in, stuffed bytes out
 }
-res["read_over_input"] = res["read_bytes_per_launch"] / res["input_plane_bytes_per_launch"]
-path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                    "pmc_encode_4k_q5.json")
-for pth in (path, os.path.join(out, "pmc_encode_4k_q5.json")):  # gpurun_out/ travels back
-    with open(pth, "w") as f:
-        json.dump(res, f, indent=1)
-print(json.dumps(res, indent=1))
+
+
+LAUNCHES = 3  # tools/pmc_workload.py --launches default
+
+
+def _width(name):
+    for k, v in KERNEL_WIDTH.items():
+        if k in name:
+            return v
+    return (4, 4)
+
+
+def main():
+    out, cal_bytes, wls = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
+    calf = load([os.path.join(out, "calib_FETCH_SIZE")])
+    calw = load([os.path.join(out, "calib_WRITE_SIZE")])
+    per_read = {8: cal_bytes / calf["k_calib_read8"]["FETCH_SIZE"],
+                4: cal_bytes / calf["k_calib_read4"]["FETCH_SIZE"]}
+    per_write = {4: cal_bytes / calw["k_calib_write4"]["WRITE_SIZE"],
+                 1: cal_bytes / calw["k_calib_write1"]["WRITE_SIZE"]}
+    import bench
+    for wl in wls:
+        W, H, DW, DH, Q, SEG, FULL, HUFF, text = bench.WORKLOADS[wl]
+        # per launch = per submit of one segment (the workload syncs LAUNCHES submits); a
+        # kernel launched per plane (k_scale: Y, U, V) sums its dispatches of one submit
+        fetch = load_totals([os.path.join(out, f"{wl}_FETCH_SIZE")])
+        write = load_totals([os.path.join(out, f"{wl}_WRITE_SIZE")])
+        kernels = {}
+        for name in sorted(set(fetch) | set(write)):
+            rw, ww = _width(name)
+            f = fetch.get(name, {}).get("FETCH_SIZE", 0.0) / LAUNCHES
+            wv = write.get(name, {}).get("WRITE_SIZE", 0.0) / LAUNCHES
+            nd = max(fetch.get(name, {}).get("dispatches", 0), write.get(name, {}).get("dispatches", 0))
+            kernels[name] = {"FETCH_SIZE": f, "WRITE_SIZE": wv, "read_width": rw, "write_width": ww,
+                             "dispatches_per_launch": nd / LAUNCHES,
+                             "read_bytes_per_launch": f * per_read[rw],
+                             "write_bytes_per_launch": wv * per_write[ww],
+                             "hbm_bytes_per_launch": f * per_read[rw] + wv * per_write[ww]}
+        in_bytes = SEG * (W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2))
+        res = {"workload": {"name": wl, "text": text, "frames_per_launch": SEG, "width": W, "height": H,
+                            "dst_width": DW, "dst_height": DH, "qscale": Q, "huffman": HUFF,
+                            "input": "testsrc2-like (tools/pmc_workload.py)"},
+               "calibration": {"kernel": "tools/calib_fetch.hip", "bytes": cal_bytes,
+                               "fetch_bytes_per_unit": per_read, "write_bytes_per_unit": per_write},
+               "input_plane_bytes_per_launch": in_bytes,
+               "kernels": kernels}
+        for pth in (os.path.join(ROOT, "profiles", f"pmc_{wl}.json"), os.path.join(out, f"pmc_{wl}.json")):
+            with open(pth, "w") as fo:
+                json.dump(res, fo, indent=1)
+        print(wl, json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 1) for k, v in kernels.items()}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,17 +1,25 @@
 #!/bin/bash
-# GPU-box job: HBM traffic of k_encode per launch from rocprofv3 PMC counters.
-#   pass 1: FETCH_SIZE of a calibration kernel reading a known byte count with the
-#           same 8-byte-per-lane width k_encode uses  -> bytes per FETCH_SIZE unit
-#   pass 2: FETCH_SIZE of the bench workload (k_encode)
-#   pass 3: WRITE_SIZE of the bench workload
-# then tools/pmc_traffic.py writes profiles/pmc_encode_4k_q5.json.
+# GPU-box job: HBM traffic per launch of every encoder kernel from rocprofv3 PMC counters.
+#   calibration: FETCH_SIZE / WRITE_SIZE of tools/calib_fetch.hip (known byte counts at the
+#                access widths the encoder uses: 8 B and 4 B reads, 4 B and 1 B writes)
+#   per workload (bench.py --workload): one FETCH_SIZE pass and one WRITE_SIZE pass (the two
+#   cannot share a pass: FETCH_SIZE takes 3 TCC counters, WRITE_SIZE 2)
+# then tools/pmc_traffic.py writes profiles/pmc_<workload>.json.
+# Usage: bash tools/pmc_traffic.sh [WORKLOAD ...]   (default: c2 c1 c4 c5)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_traffic
 mkdir -p $OUT
+WLS=${@:-c2 c1 c4 c5}
+CAL=1565523968
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o $OUT/calib_bin tools/calib_fetch.hip || exit 1
-timeout -k 10 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/calib -o run --output-format csv -- $OUT/calib_bin 1565523968 > $OUT/calib.log 2>&1 || exit 1
-timeout -k 10 150 rocprofv3 --kernel-include-regex 'mjg::' --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 tools/pmc_workload.py > $OUT/fetch.log 2>&1 || exit 1
-timeout -k 10 150 rocprofv3 --kernel-include-regex 'mjg::' --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 tools/pmc_workload.py > $OUT/write.log 2>&1 || exit 1
-python3 tools/pmc_traffic.py $OUT 1565523968 && rm -f $OUT/calib_bin && echo done
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 90 rocprofv3 --pmc $c -d $OUT/calib_$c -o run --output-format csv -- $OUT/calib_bin $CAL > $OUT/calib_$c.log 2>&1 || exit 1
+done
+for w in $WLS; do
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 150 rocprofv3 --kernel-include-regex 'mjg::' --pmc $c -d $OUT/${w}_$c -o run --output-format csv -- python3 tools/pmc_workload.py --workload $w > $OUT/${w}_$c.log 2>&1 || exit 1
+  done
+done
+python3 tools/pmc_traffic.py $OUT $CAL $WLS && rm -f $OUT/calib_bin && echo done

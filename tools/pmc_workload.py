@@ -1,39 +1,41 @@
 #!/usr/bin/env python3
-"""Small fixed workload for rocprofv3 PMC passes: 4K testsrc2-like yuv420p, q=5,
-`--launches` launches of `--frames` resident frames through k_encode and friends."""
+"""Small fixed workload for rocprofv3 PMC passes: one BASELINE config of bench.py
+(`--workload c2|c1|c4|c5`), `--launches` submits of one segment of resident frames, each
+synced before the next (so no two kernels of the encoder overlap)."""
 import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--frames", type=int, default=120)
+    p.add_argument("--workload", default="c2")
+    p.add_argument("--content", default="testsrc")
     p.add_argument("--launches", type=int, default=3)
-    p.add_argument("--w", type=int, default=3840)
-    p.add_argument("--h", type=int, default=2160)
-    p.add_argument("--q", type=int, default=5)
-    p.add_argument("--dw", type=int, default=None, help="scaled width (-vf scale)")
-    p.add_argument("--dh", type=int, default=None)
     a = p.parse_args()
     import torch
+    import bench
     from ffmpeg_distributed_amd.encoder import MjpegEncoder
-    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    from ffmpeg_distributed_amd.testsrc import CONTENT
+    W, H, DW, DH, Q, SEG, FULL, HUFF, _ = bench.WORKLOADS[a.workload]
     dev = torch.device("cuda", 0)
-    fb = a.w * a.h + 2 * ((a.w + 1) // 2) * ((a.h + 1) // 2)
-    pool = torch.empty((a.frames, fb), dtype=torch.uint8, device=dev)
-    for i in range(0, a.frames, 20):
-        k = min(20, a.frames - i)
-        pool[i:i + k] = testsrc2_i420_torch(a.w, a.h, i, k, dev)
+    fb = W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)
+    pool = torch.empty((SEG, fb), dtype=torch.uint8, device=dev)
+    gen = CONTENT[a.content]
+    for i in range(0, SEG, 10):
+        k = min(10, SEG - i)
+        pool[i:i + k] = gen(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
-    enc = MjpegEncoder(0, a.w, a.h, dst_w=a.dw, dst_h=a.dh, qscale=a.q, max_batch=a.frames)
+    enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF)
     tot = 0
     for _ in range(a.launches):
-        enc.submit(device_ptr=pool.data_ptr(), nframes=a.frames)
+        enc.submit(device_ptr=pool.data_ptr(), nframes=SEG)
         tot += int(enc.sync().sum())
-    print(f"frames/launch {a.frames} launches {a.launches} mean_jpeg {tot / a.launches / a.frames:.1f}")
+    print(f"workload {a.workload} content {a.content} frames/launch {SEG} launches {a.launches} "
+          f"mean_jpeg {tot / a.launches / SEG:.1f}")
     enc.close()
 
 
