@@ -13,6 +13,7 @@
 #include "jpeg_tables.h"
 #include "kernels.hip"
 #include "scale.hip"
+#include "fused.hip"
 #include "sws_filter.h"
 
 using namespace mjg;
@@ -152,6 +153,11 @@ struct PlaneScale {
   ScaleGeom g{};
   size_t lds = 0;
   dim3 grid;
+  // k_scale_encode tables (kFusedTabWords per entry): h per scaled column: D4 words, [6] tap
+  // position, [7] tap sum; v per scaled row: [0] first row pair, [1..npv] coefficient pairs
+  uint32_t *d_fh = nullptr, *d_fv = nullptr;
+  std::vector<uint32_t> fh, fv;
+  bool fusable = false;  // taps fit the fused kernel (HT 4/8, D4, windows inside the rows)
 };
 
 // Per-submit state.  A context has two slots so a second mjg_submit can be queued before
@@ -207,6 +213,9 @@ struct mjg_ctx {
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
+  bool fused = false;   // -vf scale through k_scale_encode (no d_scaled)
+  FusedGeom fgeom{};
+  int fused_grid = 0;   // persistent k_scale_encode workgroups
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
 
   Slot slot[2];
@@ -229,8 +238,8 @@ void free_ctx(mjg_ctx *c) {
   if (c->tail) (void)hipStreamSynchronize(c->tail);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_stage_bits, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
-                  c->ps[0].hsum, c->ps[1].hsum,
-                  c->ps[1].vps};
+                  c->ps[0].hsum, c->ps[1].hsum, c->ps[1].vps, c->ps[0].d_fh, c->ps[0].d_fv,
+                  c->ps[1].d_fh, c->ps[1].d_fv};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
@@ -312,6 +321,20 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
       const uint16_t c1 = (j1 >= 0 && j1 < vt) ? (uint16_t)p.vf.coeff[(size_t)y * vt + j1] : 0;
       vcp[(size_t)y * npv + k] = (int32_t)((uint32_t)c0 | ((uint32_t)c1 << 16));
     }
+  }
+  // fused tables
+  p.fusable = p.d4 && (ht == 8 || ht == 4) && npv <= ht / 2 + 1;  // v pairs zero-padded to HT/2 + 1
+  p.fh.assign((size_t)dw * kFusedTabWords, 0u);
+  p.fv.assign((size_t)dh * kFusedTabWords, 0u);
+  for (int x = 0; x < dw; x++) {
+    for (int k = 0; k < ht / 2 && k < 6; k++) p.fh[(size_t)x * kFusedTabWords + k] = (uint32_t)hcp[(size_t)x * (ht / 2) + k];
+    p.fh[(size_t)x * kFusedTabWords + 6] = (uint32_t)p.hf.pos[x];
+    p.fh[(size_t)x * kFusedTabWords + 7] = (uint32_t)hsum[x];
+    if (p.hf.pos[x] + ht > sw) p.fusable = false;  // the 8-byte tap window stays inside its row
+  }
+  for (int y = 0; y < dh; y++) {
+    p.fv[(size_t)y * kFusedTabWords] = (uint32_t)vps[y];
+    for (int k = 0; k < npv && k < 7; k++) p.fv[(size_t)y * kFusedTabWords + 1 + k] = (uint32_t)vcp[(size_t)y * npv + k];
   }
   int max_pairs = 0, max_nw = 0;
   for (int y0 = 0; y0 < dh; y0 += kScaleTileH) {
@@ -536,7 +559,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->timing = (k.flags & (MJG_F_TIMING | MJG_F_TIMING_DETAIL)) != 0;
   c->timing_detail = (k.flags & MJG_F_TIMING_DETAIL) != 0;
   if ((rc = alloc_slot(c, c->slot[0]))) return rc;
-  if (c->scale && (rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) return rc;
   HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
 
@@ -557,15 +579,64 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       sg.d_fstride = (long long)c->enc_frame_bytes;
       sg.range = k.in_full_range ? 0 : (p ? 2 : 1);
     }
+    // k_scale_encode: 4:2:0, one entropy-coded segment per frame (its 32-MCU groups are whole
+    // chunks), filters it handles (HT 8 / 4 with D4 coefficients), row pairs within its
+    // h-buffer; otherwise k_scale + k_encode (MJG_F_UNFUSED asks for that path)
+    c->fused = cf == MJG_CHROMA_420 && !c->rst && !(k.flags & (MJG_F_UNFUSED | MJG_F_DEBUG_COEFS)) &&
+               c->ps[0].fusable && c->ps[1].fusable && c->ps[0].g.htaps == c->ps[1].g.htaps;
+    if (c->fused) {
+      FusedGeom &fg = c->fgeom;
+      for (int p = 0; p < 2; p++) {
+        const ScaleGeom &sg = c->ps[p].g;
+        fg.sw[p] = sg.sw;
+        fg.sh[p] = sg.sh;
+        fg.dw[p] = sg.dw;
+        fg.dh[p] = sg.dh;
+        const int rows = p ? 8 : 16;  // scaled rows per MCU row
+        int np = 0;
+        for (int y0 = 0; y0 < sg.dh; y0 += rows) {
+          const int ya = y0, yb = std::min(y0 + rows - 1, sg.dh - 1);
+          np = std::max(np, (int)c->ps[p].fv[(size_t)yb * kFusedTabWords] + sg.htaps / 2 + 1 -
+                                (int)c->ps[p].fv[(size_t)ya * kFusedTabWords]);
+        }
+        fg.npairs[p] = np;
+        if (np > kFusedMaxPairs) c->fused = false;
+      }
+      fg.s_fstride = (long long)c->in_frame_bytes;
+      fg.s_off[0] = 0;
+      fg.s_off[1] = (long long)k.src_w * k.src_h;
+      fg.s_off[2] = fg.s_off[1] + (long long)scw * sch;
+      fg.gpf = (g.nmcu + kGroupMcus - 1) / kGroupMcus;
+      fg.groups_per_wg = kFusedGroupsPerWg;
+    }
+    if (c->fused) {
+      for (int p = 0; p < 2; p++) {
+        PlaneScale &ps = c->ps[p];
+        if ((rc = dmalloc(&ps.d_fh, ps.fh.size())) || (rc = dmalloc(&ps.d_fv, ps.fv.size()))) return rc;
+        HIP_TRY(hipMemcpy(ps.d_fh, ps.fh.data(), ps.fh.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ps.d_fv, ps.fv.data(), ps.fv.size() * 4, hipMemcpyHostToDevice));
+      }
+    } else if ((rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) {
+      return rc;
+    }
   }
 
-  // persistent k_encode grid: every CU filled with as many workgroups as fit
+  // persistent k_encode / k_scale_encode grids: every CU filled with as many workgroups as fit
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
+  size_t stage_cols = (size_t)c->enc_grid * kWavesPerWg;
+  if (c->fused) {
+    int fper = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &fper, c->optimal ? (const void *)k_scale_encode<8, 5, true, kCount> : (const void *)k_scale_encode<8, 5, true, kEmitDefault>,
+        64 * kFusedWaves, 0));
+    c->fused_grid = std::max(1, ncu * std::max(1, fper));
+    stage_cols = std::max(stage_cols, (size_t)c->fused_grid * kFusedWaves);
+  }
   {
-    const int rc2 = dmalloc(&c->d_stage_bits, (size_t)c->enc_grid * kWavesPerWg * 64 * kStageWords);
+    const int rc2 = dmalloc(&c->d_stage_bits, stage_cols * 64 * kStageWords);
     if (rc2) return rc2;
   }
 
@@ -605,6 +676,23 @@ int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
   HIP_TRY(hipMemcpyAsync(S.h_status, S.d_status, 4, hipMemcpyDeviceToHost, c->tail));
   HIP_TRY(hipEventRecord(S.done, c->tail));
   return MJG_OK;
+}
+
+template <int HT, int NPV, bool RANGE_ON, int MODE>
+void launch_fused3(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
+  k_scale_encode<HT, NPV, RANGE_ON, MODE><<<c->fused_grid, 64 * kFusedWaves, 0, c->stream>>>(
+      src, c->geom, c->fgeom, c->d_tabs, (const uint32_t *)c->ps[0].d_fh, (const uint32_t *)c->ps[0].d_fv,
+      (const uint32_t *)c->ps[1].d_fh, (const uint32_t *)c->ps[1].d_fv, S.d_scratch, S.d_chunk_bits,
+      c->d_stage_bits, S.d_work, n, S.d_hist, S.d_syms, S.d_symn);
+}
+
+template <int MODE>
+void launch_fused(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
+  const bool range = !c->cfg.in_full_range;
+  if (c->ps[0].g.htaps == 8)
+    range ? launch_fused3<8, 5, true, MODE>(c, S, src, n) : launch_fused3<8, 5, false, MODE>(c, S, src, n);
+  else
+    range ? launch_fused3<4, 3, true, MODE>(c, S, src, n) : launch_fused3<4, 3, false, MODE>(c, S, src, n);
 }
 
 template <int MODE>
@@ -685,7 +773,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     src = c->d_stage;
   }
   const uint8_t *enc_in = src;
-  if (c->scale) {
+  if (c->scale && !c->fused) {
     tmark(c, S, MJG_K_SCALE, 0);
     const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
     for (int p = 0; p < 3; p++) {
@@ -738,7 +826,10 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (c->optimal) {  // pass 1: symbol counts per frame, then the frame's tables
     tmark(c, S, MJG_K_HUFF, 0);
     HIP_TRY(hipMemsetAsync(S.d_hist, 0, (size_t)n * kFrameTabWords * 4, c->stream));
-    launch_encode<kCount>(c, S, enc_in, wgs, ntasks);
+    if (c->fused)
+      launch_fused<kCount>(c, S, src, n);
+    else
+      launch_encode<kCount>(c, S, enc_in, wgs, ntasks);
     HIP_TRY(hipMemsetAsync(S.d_work, 0, 4, c->stream));  // batch counter for pass 2
     k_huff_build<<<n * 4, 64, 0, c->stream>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
     tmark(c, S, MJG_K_HUFF, 1);
@@ -749,6 +840,8 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, c->stream>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
                                                                   S.d_scratch, S.d_chunk_bits, c->d_stage_bits,
                                                                   ntasks);
+  else if (c->fused)
+    launch_fused<kEmitDefault>(c, S, src, n);
   else
     launch_encode<kEmitDefault>(c, S, enc_in, wgs, ntasks);
   tmark(c, S, MJG_K_ENCODE, 1);
@@ -820,7 +913,7 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
     }
     if (c->timing) {
       for (int k = 0; k < MJG_NUM_KERNELS; k++) {
-        if (k == MJG_K_SCALE && !c->scale) continue;
+        if (k == MJG_K_SCALE && (!c->scale || c->fused)) continue;
         if (k == MJG_K_HUFF && !c->optimal) continue;
         const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
         if (tail != c->timing_detail && (tail || k == MJG_K_TAIL)) continue;
@@ -951,7 +1044,7 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
 
 int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale");
+  if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale, or scales fused (open it with MJG_F_UNFUSED)");
   if (c->nout > 0) {  // the scaled planes are shared by the slots: only the latest submit's
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;

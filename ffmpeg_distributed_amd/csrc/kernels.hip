@@ -544,6 +544,189 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
   if (lane == 0) *chunk_bits_t = total;
 }
 
+// Row pass of one chunk, lane = block: raw rows (8 little-endian words of 8 pixels) ->
+// the wave's LDS row image s_pk ([word][lane], u16 pairs of value + 32768).
+template <bool RC>
+__device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, const uint8_t *s_rc,
+                                         uint32_t *s_pk, int lane) {
+  // Row pass (jfdctint pass 1) in fp32, exactly: every value is an integer or a multiple
+  // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
+  // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
+  // (M' = 1.5*2^23 + 32768), which also leaves x + 32768 in the low 16 mantissa bits:
+  // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
+  // [RC] swscale tv->pc per pixel from a 512-byte LDS table (clip_u8((p * A21 - B21) >> 21),
+  // checked exhaustively in tests/test_oracle.py), OR'ed into the mantissa of M = 1.5*2^23:
+  // values then carry the +M bias, which the butterfly's differences cancel and its sums
+  // remove with one -2M.
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
+    float p[8];
+    p[0] = (float)((lo >> 0) & 255u);  // v_cvt_f32_ubyte0
+    p[1] = (float)((lo >> 8) & 255u);  // v_cvt_f32_ubyte1
+    p[2] = (float)((lo >> 16) & 255u);  // v_cvt_f32_ubyte2
+    p[3] = (float)((lo >> 24) & 255u);  // v_cvt_f32_ubyte3
+    p[4] = (float)((hi >> 0) & 255u);  // v_cvt_f32_ubyte0
+    p[5] = (float)((hi >> 8) & 255u);  // v_cvt_f32_ubyte1
+    p[6] = (float)((hi >> 16) & 255u);  // v_cvt_f32_ubyte2
+    p[7] = (float)((hi >> 24) & 255u);  // v_cvt_f32_ubyte3
+    float t0, t1, t2, t3;
+    if (RC) {
+      // LDS address (tab << 8) | pixel in one v_perm, the table byte OR'ed into kM's
+      // mantissa: the fp32 value kM + range(p)
+#pragma unroll
+      for (int x = 0; x < 8; x++) {
+        const uint32_t a = __builtin_amdgcn_perm((uint32_t)tab, x < 4 ? lo : hi,
+                                                 0x0c0c0400u | (uint32_t)(x & 3));
+        p[x] = __uint_as_float(0x4B400000u | (uint32_t)s_rc[a]);
+      }
+      t0 = (p[0] - 2.0f * kM) + p[7];
+      t1 = (p[1] - 2.0f * kM) + p[6];
+      t2 = (p[2] - 2.0f * kM) + p[5];
+      t3 = (p[3] - 2.0f * kM) + p[4];
+    } else {
+      t0 = p[0] + p[7];
+      t1 = p[1] + p[6];
+      t2 = p[2] + p[5];
+      t3 = p[3] + p[4];
+    }
+    const float t7 = p[0] - p[7], t6 = p[1] - p[6], t5 = p[2] - p[5], t4 = p[3] - p[4];
+    const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+    float o[8];
+    o[0] = __builtin_fmaf(t10 + t11, 16.0f, kMb);
+    o[4] = __builtin_fmaf(t10 - t11, 16.0f, kMb);
+    o[2] = __builtin_fmaf(t13, 10703.0f / 512, __builtin_fmaf(t12, 4433.0f / 512, kRnd)) + kMb;
+    o[6] = __builtin_fmaf(t13, 4433.0f / 512, __builtin_fmaf(t12, -10704.0f / 512, kRnd)) + kMb;
+    o[1] = __builtin_fmaf(t7, 11363.0f / 512, __builtin_fmaf(t6, 9633.0f / 512,
+           __builtin_fmaf(t5, 6437.0f / 512, __builtin_fmaf(t4, 2260.0f / 512, kRnd)))) + kMb;
+    o[3] = __builtin_fmaf(t7, 9633.0f / 512, __builtin_fmaf(t6, -2259.0f / 512,
+           __builtin_fmaf(t5, -11362.0f / 512, __builtin_fmaf(t4, -6436.0f / 512, kRnd)))) + kMb;
+    o[5] = __builtin_fmaf(t7, 6437.0f / 512, __builtin_fmaf(t6, -11362.0f / 512,
+           __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMb;
+    o[7] = __builtin_fmaf(t7, 2260.0f / 512, __builtin_fmaf(t6, -6436.0f / 512,
+           __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMb;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      s_pk[(r * 4 + j) * 64 + lane] =
+          __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
+    __builtin_amdgcn_sched_barrier(0);
+  }}
+
+  // Column pass (jfdctint pass 2) as a float *screen*: the products of pass 2 need up to
+  // 31 bits, so fp32 sums are only approximate (|error| < 2^9 before the 2^17 descale).
+  // Each AC coefficient is tested against its quantiser threshold widened by a margin
+  // (s_thr = B^2, fma(-s, s, B^2) < 0 <=> |s| > B), giving a candidate mask in zigzag
+  // order; emit_block quantises the candidates exactly from the integer row image
+  // (exact_coef).  Rows 0 and 4 (sums only) are exact, which gives the DC exactly:
+  // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
+__device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, const uint32_t *s_skip,
+                                              const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb) {
+#pragma unroll
+  for (int jp = 0; jp < 4; jp++) {
+    __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
+    uint32_t w[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
+    // Column skip (pairs 1-3): every AC output of a column quantises to zero when the
+    // column's row-pass values are small enough.  Rows 1-7 of pass 2 have coefficient
+    // sums 0, so |S_k| <= L1(row k) * R / 2 with R = max - min of the column; row 0 is
+    // the plain sum, |S_0| <= 8 max|u|.  open_ctx turns the quantiser thresholds into
+    // limits on R, max and min (u16 with the +32768 bias), tested with packed u16
+    // max/min and saturating subtracts; a column is skipped when every block of the
+    // chunk passes (wave ballot), its 8 screen bits are then 0.
+    bool skip0 = false, skip1 = false;
+    if (jp > 0) {
+      u16x2 mx = as_u16x2(w[0]), mn = mx;
+#pragma unroll
+      for (int r = 1; r < 8; r++) {
+        mx = __builtin_elementwise_max(mx, as_u16x2(w[r]));
+        mn = __builtin_elementwise_min(mn, as_u16x2(w[r]));
+      }
+      const uint32_t t =
+          as_u32(__builtin_elementwise_sub_sat(mx - mn, as_u16x2(s_skip[3 * jp - 3]))) |
+          as_u32(__builtin_elementwise_sub_sat(mx, as_u16x2(s_skip[3 * jp - 2]))) |
+          as_u32(__builtin_elementwise_sub_sat(as_u16x2(s_skip[3 * jp - 1]), mn));
+      skip0 = __ballot((t & 0xffffu) != 0u) == 0;
+      skip1 = __ballot((t >> 16) != 0u) == 0;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      __builtin_amdgcn_sched_barrier(0);  // one column at a time
+      const int col = 2 * jp + h;
+      if (h ? skip1 : skip0) {  // wave-uniform: 8 zero screen bits
+        if (col < 4)
+          ca <<= 8;
+        else
+          cb <<= 8;
+        continue;
+      }
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));
+      // x = M' + value: differences cancel the bias, sums drop it with one -2M'
+      const float t0 = (x[0] - 2.0f * kMb) + x[7], t7 = x[0] - x[7];
+      const float t1 = (x[1] - 2.0f * kMb) + x[6], t6 = x[1] - x[6];
+      const float t2 = (x[2] - 2.0f * kMb) + x[5], t5 = x[2] - x[5];
+      const float t3 = (x[3] - 2.0f * kMb) + x[4], t4 = x[3] - x[4];
+      const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+      float sv[8];
+      sv[0] = t10 + t11;
+      sv[4] = t10 - t11;
+      sv[2] = __builtin_fmaf(t13, 10703.0f, t12 * 4433.0f);
+      sv[6] = __builtin_fmaf(t13, 4433.0f, t12 * -10704.0f);
+      sv[1] = __builtin_fmaf(t7, 11363.0f, __builtin_fmaf(t6, 9633.0f, __builtin_fmaf(t5, 6437.0f, t4 * 2260.0f)));
+      sv[3] = __builtin_fmaf(t7, 9633.0f, __builtin_fmaf(t6, -2259.0f, __builtin_fmaf(t5, -11362.0f, t4 * -6436.0f)));
+      sv[5] = __builtin_fmaf(t7, 6437.0f, __builtin_fmaf(t6, -11362.0f, __builtin_fmaf(t5, 2261.0f, t4 * 9633.0f)));
+      sv[7] = __builtin_fmaf(t7, 2260.0f, __builtin_fmaf(t6, -6436.0f, __builtin_fmaf(t5, 9633.0f, t4 * -11363.0f)));
+      const float4 ta = *(const float4 *)(s_thr + col * 8), tb = *(const float4 *)(s_thr + col * 8 + 4);
+      const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        if (col == 0 && r == 0) {
+          dc = (int)(__float_as_uint(__builtin_fmaf(sv[0], 1.0f / 1024, 0x1.1p-7f) + kM) - 0x4B400000u);
+        } else {
+          // sign of B^2 - s^2 shifted into the candidate word in computation order
+          // (v_alignbit: (m << 1) | (neg >> 31)); zigzag order is restored below
+          const uint32_t neg = __float_as_uint(__builtin_fmaf(-sv[r], sv[r], thr[r]));
+          if (col < 4)
+            ca = __builtin_amdgcn_alignbit(ca, neg, 31);
+          else
+            cb = __builtin_amdgcn_alignbit(cb, neg, 31);
+        }
+      }
+    }
+  }
+}
+
+// Candidate bits (column_screen) -> zigzag-ordered candidate mask (a handful per block).
+__device__ __forceinline__ uint64_t screen_mask(uint32_t ca, uint32_t cb, const uint8_t *s_scat) {
+  uint64_t mask = 0;
+  while (ca) {
+    const int pos = __builtin_ctz(ca);
+    ca &= ca - 1;
+    mask |= 1ull << s_scat[pos];
+  }
+  while (cb) {
+    const int pos = __builtin_ctz(cb);
+    cb &= cb - 1;
+    mask |= 1ull << s_scat[32 + pos];
+  }
+  return mask;
+}
+
+// DC predictor of this lane's block (FFmpeg last_dc, 128 at every segment start): the block
+// `delta` before it in coding order (the previous block of the same component) is in this
+// chunk (lane - delta) or among the previous chunk's last 8 blocks, whose DCs lanes 56..63
+// carry.  One bpermute for both: quantised DCs and carried DCs fit int16.
+__device__ __forceinline__ int dc_predictor(int dc, int carry, int delta, bool first_chunk, int lane) {
+  const int src_lane = (lane - delta) & 63;
+  const uint32_t both = __builtin_amdgcn_ds_bpermute(
+      src_lane << 2, (int)(((uint32_t)dc & 0xffffu) | ((uint32_t)carry << 16)));
+  const int from_cur = (int)(int16_t)(both & 0xffffu), from_prev = (int)both >> 16;
+  return lane >= delta ? from_cur : (first_chunk ? 128 : from_prev);
+}
+
 template <bool RC, int MODE>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
@@ -616,68 +799,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint32_t dsc = s_desc[block_in_mcu(g, b)];
     const int tab = desc_tab(dsc);
     if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, bbase + b, s_desc));
-    // Row pass (jfdctint pass 1) in fp32, exactly: every value is an integer or a multiple
-    // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
-    // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
-    // (M' = 1.5*2^23 + 32768), which also leaves x + 32768 in the low 16 mantissa bits:
-    // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
-    // [RC] swscale tv->pc per pixel from a 512-byte LDS table (clip_u8((p * A21 - B21) >> 21),
-    // checked exhaustively in tests/test_oracle.py), OR'ed into the mantissa of M = 1.5*2^23:
-    // values then carry the +M bias, which the butterfly's differences cancel and its sums
-    // remove with one -2M.
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
-      float p[8];
-      p[0] = (float)((lo >> 0) & 255u);  // v_cvt_f32_ubyte0
-      p[1] = (float)((lo >> 8) & 255u);  // v_cvt_f32_ubyte1
-      p[2] = (float)((lo >> 16) & 255u);  // v_cvt_f32_ubyte2
-      p[3] = (float)((lo >> 24) & 255u);  // v_cvt_f32_ubyte3
-      p[4] = (float)((hi >> 0) & 255u);  // v_cvt_f32_ubyte0
-      p[5] = (float)((hi >> 8) & 255u);  // v_cvt_f32_ubyte1
-      p[6] = (float)((hi >> 16) & 255u);  // v_cvt_f32_ubyte2
-      p[7] = (float)((hi >> 24) & 255u);  // v_cvt_f32_ubyte3
-      float t0, t1, t2, t3;
-      if (rc) {
-        // LDS address (tab << 8) | pixel in one v_perm, the table byte OR'ed into kM's
-        // mantissa: the fp32 value kM + range(p)
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-          const uint32_t a = __builtin_amdgcn_perm((uint32_t)tab, x < 4 ? lo : hi,
-                                                   0x0c0c0400u | (uint32_t)(x & 3));
-          p[x] = __uint_as_float(0x4B400000u | (uint32_t)s_rc[a]);
-        }
-        t0 = (p[0] - 2.0f * kM) + p[7];
-        t1 = (p[1] - 2.0f * kM) + p[6];
-        t2 = (p[2] - 2.0f * kM) + p[5];
-        t3 = (p[3] - 2.0f * kM) + p[4];
-      } else {
-        t0 = p[0] + p[7];
-        t1 = p[1] + p[6];
-        t2 = p[2] + p[5];
-        t3 = p[3] + p[4];
-      }
-      const float t7 = p[0] - p[7], t6 = p[1] - p[6], t5 = p[2] - p[5], t4 = p[3] - p[4];
-      const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
-      float o[8];
-      o[0] = __builtin_fmaf(t10 + t11, 16.0f, kMb);
-      o[4] = __builtin_fmaf(t10 - t11, 16.0f, kMb);
-      o[2] = __builtin_fmaf(t13, 10703.0f / 512, __builtin_fmaf(t12, 4433.0f / 512, kRnd)) + kMb;
-      o[6] = __builtin_fmaf(t13, 4433.0f / 512, __builtin_fmaf(t12, -10704.0f / 512, kRnd)) + kMb;
-      o[1] = __builtin_fmaf(t7, 11363.0f / 512, __builtin_fmaf(t6, 9633.0f / 512,
-             __builtin_fmaf(t5, 6437.0f / 512, __builtin_fmaf(t4, 2260.0f / 512, kRnd)))) + kMb;
-      o[3] = __builtin_fmaf(t7, 9633.0f / 512, __builtin_fmaf(t6, -2259.0f / 512,
-             __builtin_fmaf(t5, -11362.0f / 512, __builtin_fmaf(t4, -6436.0f / 512, kRnd)))) + kMb;
-      o[5] = __builtin_fmaf(t7, 6437.0f / 512, __builtin_fmaf(t6, -11362.0f / 512,
-             __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMb;
-      o[7] = __builtin_fmaf(t7, 2260.0f / 512, __builtin_fmaf(t6, -6436.0f / 512,
-             __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMb;
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        s_pk[(r * 4 + j) * 64 + lane] =
-            __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    row_pass<RC>(raw, tab, s_rc, s_pk, lane);
     // prefetch the next chunk while this one is encoded
     const int cur_frame = frame, cur_chunk = chunk, cur_bbase = bbase;
     const bool cur_active = active;
@@ -696,92 +818,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
     const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, bbase, chunk, lane, s_desc) : 0;
 
-    // Column pass (jfdctint pass 2) as a float *screen*: the products of pass 2 need up to
-    // 31 bits, so fp32 sums are only approximate (|error| < 2^9 before the 2^17 descale).
-    // Each AC coefficient is tested against its quantiser threshold widened by a margin
-    // (s_thr = B^2, fma(-s, s, B^2) < 0 <=> |s| > B), giving a candidate mask in zigzag
-    // order; emit_block quantises the candidates exactly from the integer row image
-    // (exact_coef).  Rows 0 and 4 (sums only) are exact, which gives the DC exactly:
-    // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
     int dc = 0;
     uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
     if (cur_active) {
-#pragma unroll
-      for (int jp = 0; jp < 4; jp++) {
-        __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
-        uint32_t w[8];
-#pragma unroll
-        for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
-        // Column skip (pairs 1-3): every AC output of a column quantises to zero when the
-        // column's row-pass values are small enough.  Rows 1-7 of pass 2 have coefficient
-        // sums 0, so |S_k| <= L1(row k) * R / 2 with R = max - min of the column; row 0 is
-        // the plain sum, |S_0| <= 8 max|u|.  open_ctx turns the quantiser thresholds into
-        // limits on R, max and min (u16 with the +32768 bias), tested with packed u16
-        // max/min and saturating subtracts; a column is skipped when every block of the
-        // chunk passes (wave ballot), its 8 screen bits are then 0.
-        bool skip0 = false, skip1 = false;
-        if (jp > 0) {
-          u16x2 mx = as_u16x2(w[0]), mn = mx;
-#pragma unroll
-          for (int r = 1; r < 8; r++) {
-            mx = __builtin_elementwise_max(mx, as_u16x2(w[r]));
-            mn = __builtin_elementwise_min(mn, as_u16x2(w[r]));
-          }
-          const uint32_t t =
-              as_u32(__builtin_elementwise_sub_sat(mx - mn, as_u16x2(s_skip[3 * jp - 3]))) |
-              as_u32(__builtin_elementwise_sub_sat(mx, as_u16x2(s_skip[3 * jp - 2]))) |
-              as_u32(__builtin_elementwise_sub_sat(as_u16x2(s_skip[3 * jp - 1]), mn));
-          skip0 = __ballot((t & 0xffffu) != 0u) == 0;
-          skip1 = __ballot((t >> 16) != 0u) == 0;
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          __builtin_amdgcn_sched_barrier(0);  // one column at a time
-          const int col = 2 * jp + h;
-          if (h ? skip1 : skip0) {  // wave-uniform: 8 zero screen bits
-            if (col < 4)
-              ca <<= 8;
-            else
-              cb <<= 8;
-            continue;
-          }
-          float x[8];
-#pragma unroll
-          for (int r = 0; r < 8; r++)
-            x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));
-          // x = M' + value: differences cancel the bias, sums drop it with one -2M'
-          const float t0 = (x[0] - 2.0f * kMb) + x[7], t7 = x[0] - x[7];
-          const float t1 = (x[1] - 2.0f * kMb) + x[6], t6 = x[1] - x[6];
-          const float t2 = (x[2] - 2.0f * kMb) + x[5], t5 = x[2] - x[5];
-          const float t3 = (x[3] - 2.0f * kMb) + x[4], t4 = x[3] - x[4];
-          const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
-          float sv[8];
-          sv[0] = t10 + t11;
-          sv[4] = t10 - t11;
-          sv[2] = __builtin_fmaf(t13, 10703.0f, t12 * 4433.0f);
-          sv[6] = __builtin_fmaf(t13, 4433.0f, t12 * -10704.0f);
-          sv[1] = __builtin_fmaf(t7, 11363.0f, __builtin_fmaf(t6, 9633.0f, __builtin_fmaf(t5, 6437.0f, t4 * 2260.0f)));
-          sv[3] = __builtin_fmaf(t7, 9633.0f, __builtin_fmaf(t6, -2259.0f, __builtin_fmaf(t5, -11362.0f, t4 * -6436.0f)));
-          sv[5] = __builtin_fmaf(t7, 6437.0f, __builtin_fmaf(t6, -11362.0f, __builtin_fmaf(t5, 2261.0f, t4 * 9633.0f)));
-          sv[7] = __builtin_fmaf(t7, 2260.0f, __builtin_fmaf(t6, -6436.0f, __builtin_fmaf(t5, 9633.0f, t4 * -11363.0f)));
-          const float4 ta = *(const float4 *)(s_thr + col * 8), tb = *(const float4 *)(s_thr + col * 8 + 4);
-          const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
-#pragma unroll
-          for (int r = 0; r < 8; r++) {
-            if (col == 0 && r == 0) {
-              dc = (int)(__float_as_uint(__builtin_fmaf(sv[0], 1.0f / 1024, 0x1.1p-7f) + kM) - 0x4B400000u);
-            } else {
-              // sign of B^2 - s^2 shifted into the candidate word in computation order
-              // (v_alignbit: (m << 1) | (neg >> 31)); zigzag order is restored below
-              const uint32_t neg = __float_as_uint(__builtin_fmaf(-sv[r], sv[r], thr[r]));
-              if (col < 4)
-                ca = __builtin_amdgcn_alignbit(ca, neg, 31);
-              else
-                cb = __builtin_amdgcn_alignbit(cb, neg, 31);
-            }
-          }
-        }
-      }
+      column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
       if (g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
@@ -793,29 +833,11 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
         }
       }
     }
-    // candidate bits -> zigzag-ordered mask (a handful of candidates per block)
-    uint64_t mask = 0;
-    while (ca) {
-      const int pos = __builtin_ctz(ca);
-      ca &= ca - 1;
-      mask |= 1ull << s_scat[pos];
-    }
-    while (cb) {
-      const int pos = __builtin_ctz(cb);
-      cb &= cb - 1;
-      mask |= 1ull << s_scat[32 + pos];
-    }
+    const uint64_t mask = screen_mask(ca, cb, s_scat);
 
     // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.
-    const int delta = desc_delta(dsc);
-    const int src_lane = (lane - delta) & 63;
-    // one bpermute for both: quantised DCs and carried DCs fit int16
-    const uint32_t both = __builtin_amdgcn_ds_bpermute(
-        src_lane << 2, (int)(((uint32_t)dc & 0xffffu) | ((uint32_t)carry << 16)));
-    const int from_cur = (int)(int16_t)(both & 0xffffu), from_prev = (int)both >> 16;
-    const int pred = lane >= delta ? from_cur : (cur_chunk == 0 ? 128 : from_prev);
-    const int diff = dc - pred;
+    const int diff = dc - dc_predictor(dc, carry, desc_delta(dsc), cur_chunk == 0, lane);
     carry = dc;
 
     if (MODE == kCount && cur_frame != aux_frame) {  // flush the previous frame's counts

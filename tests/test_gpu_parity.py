@@ -204,7 +204,7 @@ def test_scale_matches_oracle(sw, sh, dw, dh, full):
     kind = "testsrc" if sw >= 1000 else "smooth"
     frames = rand_frames(sw, sh, n, seed=11, kind=kind)
     q = 3
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2) as enc:
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, unfused=True) as enc:
         enc.submit(frames)
         enc.sync()
         planes = [enc.debug_planes(i) for i in range(n)]
@@ -225,6 +225,59 @@ def test_scale_matches_oracle(sw, sh, dw, dh, full):
         gy, gu, gv = split_i420(planes[i], dw, dh)
         assert (gy == ry).all() and (gu == ru).all() and (gv == rv).all()
     assert got == oracle_frames(frames, sw, sh, q, full, dw, dh)
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2) as enc:
+        assert enc.encode(frames) == got  # the fused k_scale_encode path (where it applies)
+
+
+FUSED_CASES = [
+    # (sw, sh, dw, dh, q, full, kind, n, huffman): fused k_scale_encode vs the oracle
+    (3840, 2160, 1920, 1080, 3, False, "testsrc", 3, "default"),   # BASELINE configs[3]
+    (3840, 2160, 1920, 1080, 3, True, "noise", 2, "default"),
+    (3840, 2160, 1920, 1080, 5, False, "testsrc", 2, "optimal"),
+    (1920, 1080, 1280, 720, 4, False, "smooth", 2, "default"),      # 1.5:1
+    (1280, 720, 640, 360, 2, True, "patches", 3, "default"),
+    (640, 360, 1280, 720, 5, False, "testsrc", 2, "default"),       # upscale: 4 taps
+    (400, 300, 200, 150, 6, False, "checker", 3, "optimal"),        # 13 MCUs per row: groups span rows
+    (96, 64, 48, 32, 3, True, "noise", 2, "default"),               # one partial group
+    (130, 98, 66, 50, 5, False, "smooth", 3, "default"),            # odd sizes, edge MCUs
+    (2200, 1300, 1100, 650, 7, False, "patches", 1, "default"),     # nmcu % 32 != 0
+]
+
+
+@pytest.mark.parametrize("sw,sh,dw,dh,q,full,kind,n,huffman", FUSED_CASES)
+def test_fused_scale_encode_matches_oracle(sw, sh, dw, dh, q, full, kind, n, huffman):
+    """k_scale_encode (scaled pixels kept in LDS) byte-equal to the oracle's scale_plane +
+    encode_frame, and to the unfused k_scale + k_encode path."""
+    frames = rand_frames(sw, sh, n, seed=sw + dh + q, kind=kind)
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman) as enc:
+        got = enc.encode(frames)
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman,
+                      unfused=True) as enc:
+        got_unfused = enc.encode(frames)
+    ref = _oracle_many(frames, sw, sh, dst_w=dw, dst_h=dh, full_range=full, qscale=q, huffman=huffman)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+    assert got_unfused == got
+
+
+def test_fused_4k_segment_batch_from_device_memory():
+    """BASELINE configs[3] as bench.py submits it: 120 4K frames by device pointer through
+    the fused kernel, every frame equal to the oracle."""
+    import torch
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    w, h, n = 3840, 2160, 120
+    dev = torch.device("cuda", 0)
+    pool = torch.empty((n, i420_frame_bytes(w, h)), dtype=torch.uint8, device=dev)
+    for i in range(0, n, 20):
+        pool[i:i + 20] = testsrc2_i420_torch(w, h, 500 + i, 20, dev)
+    torch.cuda.synchronize()
+    host = pool.cpu().numpy()
+    with MjpegEncoder(0, w, h, 1920, 1080, qscale=3, max_batch=n) as enc:
+        enc.submit(device_ptr=pool.data_ptr(), nframes=n)
+        got = enc.fetch()
+    ref = _oracle_many(host, w, h, dst_w=1920, dst_h=1080, qscale=3)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
 def _oracle_many(frames, w, h, **kw):
