@@ -582,8 +582,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     // k_scale_encode: 4:2:0, one entropy-coded segment per frame (its 32-MCU groups are whole
     // chunks), filters it handles (HT 8 / 4 with D4 coefficients), row pairs within its
     // h-buffer; otherwise k_scale + k_encode (MJG_F_UNFUSED asks for that path)
+    // (>= 32 MCUs per row: a group touches at most two MCU rows, whose v rows are staged in LDS)
     c->fused = cf == MJG_CHROMA_420 && !c->rst && !(k.flags & (MJG_F_UNFUSED | MJG_F_DEBUG_COEFS)) &&
-               c->ps[0].fusable && c->ps[1].fusable && c->ps[0].g.htaps == c->ps[1].g.htaps;
+               c->ps[0].fusable && c->ps[1].fusable && c->ps[0].g.htaps == c->ps[1].g.htaps &&
+               g.mbw >= kGroupMcus;
     if (c->fused) {
       FusedGeom &fg = c->fgeom;
       for (int p = 0; p < 2; p++) {
@@ -599,6 +601,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
           np = std::max(np, (int)c->ps[p].fv[(size_t)yb * kFusedTabWords] + sg.htaps / 2 + 1 -
                                 (int)c->ps[p].fv[(size_t)ya * kFusedTabWords]);
         }
+        np = (np + kFusedBatch - 1) / kFusedBatch * kFusedBatch;  // whole load batches (extra rows: clamped, unused)
         fg.npairs[p] = np;
         if (np > kFusedMaxPairs) c->fused = false;
       }

@@ -36,7 +36,8 @@ namespace mjg {
 
 constexpr int kFusedWaves = 3;
 constexpr int kGroupMcus = 32;           // 4:2:0: 32 MCUs = 192 blocks = 3 chunks
-constexpr int kFusedMaxPairs = 21;       // h-pass row pairs per column task (2:1 luma: 20)
+constexpr int kFusedMaxPairs = 20;       // h-pass row pairs per column task (2:1 luma: 20)
+constexpr int kFusedBatch = 4;           // h-pass pairs whose loads are in flight together
 constexpr int kFusedGroupsPerWg = 4;     // consecutive groups per workgroup
 constexpr int kFusedTabWords = 8;        // words per column (h) / row (v) filter entry
 constexpr int kImgY = 16 * 512, kImgC = 8 * 256;           // LDS image bytes per plane
@@ -53,24 +54,20 @@ struct FusedGeom {
   int npairs[2];              // h-pass row pairs a column task needs, luma / chroma (<= kFusedMaxPairs)
 };
 
-// One h-pass output: hScale8To15 of the 8 (HT) taps at src (D4 words c[0..HT/2)), then the
-// range conversion.  hs = sum of the taps' coefficients (folded into the hi accumulator).
+__device__ __forceinline__ int dot4_i8(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
+
+// One h-pass output: hScale8To15 of the HT (8 or 4) taps in w (little-endian bytes, D4 words
+// c[0..HT/2)), then the range conversion.  hs = sum of the taps' coefficients (folded into
+// the hi accumulator).
 template <int HT, int RANGE>
-__device__ __forceinline__ int fused_hscale(const uint8_t *src, const uint32_t (&c)[HT / 2], int hs) {
-  typedef uint64_t u64_unaligned __attribute__((aligned(1)));
-  typedef uint32_t u32_unaligned __attribute__((aligned(1)));
-  int ah = hs, al = 0;
+__device__ __forceinline__ int fused_hscale(uint64_t w, const uint32_t (&c)[HT / 2], int hs) {
+  const int lo = (int)((uint32_t)w ^ 0x80808080u);
+  int ah = dot4_i8(lo, (int)c[0], hs);
+  int al = dot4_i8(lo, (int)c[1], 0);
   if constexpr (HT == 8) {
-    const uint64_t w = *(const u64_unaligned *)src;
-    const int lo = (int)((uint32_t)w ^ 0x80808080u), hi = (int)((uint32_t)(w >> 32) ^ 0x80808080u);
-    ah = __builtin_amdgcn_sdot4(lo, (int)c[0], ah, false);
-    al = __builtin_amdgcn_sdot4(lo, (int)c[1], al, false);
-    ah = __builtin_amdgcn_sdot4(hi, (int)c[2], ah, false);
-    al = __builtin_amdgcn_sdot4(hi, (int)c[3], al, false);
-  } else {  // HT == 4
-    const int lo = (int)(*(const u32_unaligned *)src ^ 0x80808080u);
-    ah = __builtin_amdgcn_sdot4(lo, (int)c[0], ah, false);
-    al = __builtin_amdgcn_sdot4(lo, (int)c[1], al, false);
+    const int hi = (int)((uint32_t)(w >> 32) ^ 0x80808080u);
+    ah = dot4_i8(hi, (int)c[2], ah);
+    al = dot4_i8(hi, (int)c[3], al);
   }
   const int v = ah + (al >> 7);
   if (RANGE == 1) return (__mul24(min(v, 30189), 19077) - 39057361) >> 14;  // min also clips 32767
@@ -78,62 +75,113 @@ __device__ __forceinline__ int fused_hscale(const uint8_t *src, const uint32_t (
   return min(v, 32767);
 }
 
-// One column task: lane = one scaled column `x` of plane `pl` (0 luma, 1/2 chroma), output rows
-// ybase .. ybase + rows - 1 (clamped to the plane), written as bytes to dst[i * dpitch].
-// hbuf: the wave's h-buffer ([pair][lane]).  RANGE_ON: tv input (luma 1, chroma 2 per plane).
-template <int HT, int NPV, bool RANGE_ON>
-__device__ __forceinline__ void fused_column(const uint8_t *frame, const FusedGeom &fg, int pl, int x,
-                                             int ybase, int rows, const uint32_t *__restrict__ htab,
-                                             const uint32_t *__restrict__ vtab, uint32_t *hbuf,
-                                             uint8_t *dst, int dpitch, bool valid, int lane, int np) {
-  const int pc = pl ? 1 : 0;
-  const int sw = fg.sw[pc], sh = fg.sh[pc], dh = fg.dh[pc];
-  const uint8_t *src = frame + fg.s_off[pl];
+// h-table entry of one scaled column: D4 coefficient words, tap position, tap sum.
+template <int HT>
+struct HCol {
+  uint32_t c[HT / 2];
+  int hpos, hs;
+};
+
+template <int HT>
+__device__ __forceinline__ HCol<HT> load_hcol(const uint32_t *__restrict__ htab, int x) {
   const uint32_t *ht = htab + (size_t)x * kFusedTabWords;
   const uint4 h0 = *(const uint4 *)ht, h1 = *(const uint4 *)(ht + 4);
-  uint32_t c[HT / 2];
-  c[0] = h0.x;
-  c[1] = h0.y;
+  HCol<HT> r;
+  r.c[0] = h0.x;
+  r.c[1] = h0.y;
   if constexpr (HT == 8) {
-    c[2] = h0.z;
-    c[3] = h0.w;
+    r.c[2] = h0.z;
+    r.c[3] = h0.w;
   }
-  const int hpos = (int)h1.z, hs = (int)h1.w;
+  r.hpos = (int)h1.z;
+  r.hs = (int)h1.w;
+  return r;
+}
+
+// The rows of MCU row my (wave-uniform) for this lane's column (h entry hc): the ROWS scaled
+// rows, bytes to dst[i * dpitch] when `valid`.  Everything row-related is wave-uniform: the
+// source row addresses are scalar (the loads take the lane's tap position as their only
+// vector operand) and the v rows come by scalar loads.  The tap-window loads (np <=
+// kFusedMaxPairs row pairs, 8 B each, np a multiple of kFusedBatch) go out kFusedBatch pairs
+// ahead of their use.
+template <int HT, int NPV, int RANGE, int ROWS>
+__device__ __forceinline__ void fused_rows(const uint8_t *__restrict__ src, int sw, int sh, int dh, int my,
+                                           const HCol<HT> &hc, const uint32_t *__restrict__ vtab,
+                                           uint32_t *hbuf, uint8_t *dst, int dpitch, bool valid, int lane,
+                                           int np) {
+  typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+  typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+  const int ybase = my * ROWS;
   const int ps0 = (int)vtab[(size_t)min(ybase, dh - 1) * kFusedTabWords];
-  const uint8_t *colp = src + hpos;
-  // h-pass: source rows 2 (ps0 + p) and 2 (ps0 + p) + 1 of pair p (rows past the plane meet
-  // only zero coefficients: clamped)
   const int rmax = sh - 1;
-#pragma unroll 2
-  for (int p = 0; p < np; p++) {
-    const int r0 = min(2 * (ps0 + p), rmax), r1 = min(2 * (ps0 + p) + 1, rmax);
-    int a, b;
-    if (RANGE_ON) {
-      if (pc == 0) {
-        a = fused_hscale<HT, 1>(colp + (size_t)r0 * sw, c, hs);
-        b = fused_hscale<HT, 1>(colp + (size_t)r1 * sw, c, hs);
-      } else {
-        a = fused_hscale<HT, 2>(colp + (size_t)r0 * sw, c, hs);
-        b = fused_hscale<HT, 2>(colp + (size_t)r1 * sw, c, hs);
-      }
-    } else {
-      a = fused_hscale<HT, 0>(colp + (size_t)r0 * sw, c, hs);
-      b = fused_hscale<HT, 0>(colp + (size_t)r1 * sw, c, hs);
+  const uint32_t hp = (uint32_t)hc.hpos;
+  auto load = [&](uint64_t (&w)[2 * kFusedBatch], int p0) {
+#pragma unroll
+    for (int q = 0; q < 2 * kFusedBatch; q++) {
+      const uint8_t *row = src + (size_t)min(2 * (ps0 + p0) + q, rmax) * sw;  // uniform
+      if constexpr (HT == 8)
+        w[q] = *(const u64_unaligned *)(row + hp);
+      else
+        w[q] = *(const u32_unaligned *)(row + hp);
     }
-    hbuf[p * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
+  };
+  auto compute = [&](const uint64_t (&w)[2 * kFusedBatch], int p0) {
+#pragma unroll
+    for (int k = 0; k < kFusedBatch; k++) {
+      const int a = fused_hscale<HT, RANGE>(w[2 * k], hc.c, hc.hs);
+      const int b = fused_hscale<HT, RANGE>(w[2 * k + 1], hc.c, hc.hs);
+      hbuf[(p0 + k) * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
+    }
+  };
+  // np is a multiple of kFusedBatch (host-rounded); the next batch's loads are issued before
+  // the current batch is computed
+  uint64_t wa[2 * kFusedBatch], wb[2 * kFusedBatch];
+  load(wa, 0);
+#pragma unroll 1
+  for (int p0 = 0; p0 < np; p0 += 2 * kFusedBatch) {
+    if (p0 + kFusedBatch < np) load(wb, p0 + kFusedBatch);
+    compute(wa, p0);
+    if (p0 + kFusedBatch >= np) break;
+    if (p0 + 2 * kFusedBatch < np) load(wa, p0 + 2 * kFusedBatch);
+    compute(wb, p0 + kFusedBatch);
   }
   // v-pass: output row y reads the pairs [vps[y], vps[y] + NPV) against its pair coefficients
-  for (int i = 0; i < rows; i++) {
-    const uint32_t *vr = vtab + (size_t)min(ybase + i, dh - 1) * kFusedTabWords;
-    const uint4 v0 = *(const uint4 *)vr, v1 = *(const uint4 *)(vr + 4);
-    const uint32_t vc[7] = {v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t *cp = hbuf + ((int)v0.x - ps0) * 64 + lane;
+  const uint32_t *hcol = hbuf + lane;
+#pragma unroll 2
+  for (int i = 0; i < ROWS; i++) {
+    const uint32_t *vr = vtab + (size_t)min(ybase + i, dh - 1) * kFusedTabWords;  // uniform
+    const uint32_t *cp = hcol + ((int)vr[0] - ps0) * 64;
     int acc = 64 << 12;
 #pragma unroll
     for (int k = 0; k < NPV; k++)
-      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, cp[k * 64]), __builtin_bit_cast(short2_t, vc[k]),
+      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, cp[k * 64]), __builtin_bit_cast(short2_t, vr[1 + k]),
                                    acc, false);
     if (valid) dst[i * dpitch] = (uint8_t)min(max(acc >> 19, 0), 255);
+  }
+}
+
+// One column task of plane pl (wave-uniform): lane = scaled column x of MCU (my, ...); the lanes'
+// MCU rows are run one at a time (at most two: a 64-column task straddles a row end only when
+// the MCUs per row are not a multiple of its 4 / 8 MCUs), so row work stays wave-uniform.
+template <int HT, int NPV, bool RANGE_ON>
+__device__ __forceinline__ void fused_task_rows(const uint8_t *frame, const FusedGeom &fg, int pl, int my,
+                                                const HCol<HT> &hc, const uint32_t *vtab0, const uint32_t *vtab1,
+                                                uint32_t *hbuf, uint8_t *dst, bool valid, int lane) {
+  const uint8_t *src = frame + fg.s_off[pl];
+  auto run = [&](int my_u) {
+    if (pl == 0)
+      fused_rows<HT, NPV, RANGE_ON ? 1 : 0, 16>(src, fg.sw[0], fg.sh[0], fg.dh[0], my_u, hc, vtab0, hbuf, dst, 512,
+                                                 valid, lane, fg.npairs[0]);
+    else
+      fused_rows<HT, NPV, RANGE_ON ? 2 : 0, 8>(src, fg.sw[1], fg.sh[1], fg.dh[1], my_u, hc, vtab1, hbuf, dst, 256,
+                                                valid, lane, fg.npairs[1]);
+  };
+  const int my_a = __builtin_amdgcn_readfirstlane(my);
+  if (my == my_a) run(my_a);
+  const uint64_t rest = __ballot(my != my_a);
+  if (rest) {  // the lanes of the second MCU row
+    const int my_b = __builtin_amdgcn_readlane(my, (int)__builtin_ctzll(rest));
+    if (my == my_b) run(my_b);
   }
 }
 
@@ -141,30 +189,59 @@ __device__ __forceinline__ void fused_column(const uint8_t *frame, const FusedGe
 // tasks of 64 columns (8 MCUs each).  Wave order balances the cost (a luma task scales 16
 // rows from ~40 source rows, a chroma task 8 rows from ~24): waves get {L0 L3 L6 C0 C3},
 // {L1 L4 L7 C1 C4}, {L2 L5 C2 C5 C6 C7} (C0-3 Cb, C4-7 Cr).
-__device__ static constexpr int8_t kFusedTasks[3][6] = {
-    {0, 3, 6, 8, 11, -1}, {1, 4, 7, 9, 12, -1}, {2, 5, 10, 13, 14, 15}};
+__device__ static constexpr int8_t kFusedTasks[3][7] = {
+    {0, 3, 6, 8, 11, -1, -1}, {1, 4, 7, 9, 12, -1, -1}, {2, 5, 10, 13, 14, 15, -1}};
 
+// Task t of group grp: the lane's column x, MCU row, whether its MCU is inside the frame and
+// its LDS image byte.  Plane pl = task_plane(t) is wave-uniform.
+__device__ __forceinline__ int task_plane(int t) { return t < 8 ? 0 : (t < 12 ? 1 : 2); }
+
+struct FusedTask {
+  int x, my, img_off;
+  bool valid;
+};
+
+__device__ __forceinline__ FusedTask fused_task(const EncGeom &g, const FusedGeom &fg, int grp, int t, int pl,
+                                                int lane) {
+  FusedTask r;
+  const int j = (t < 8 ? t : (t & 3)) * 64 + lane;  // column within the group's plane strip
+  const int mw = pl ? 8 : 16;                        // MCU width in this plane
+  const int ml = j / mw, m0 = grp * kGroupMcus + ml;
+  r.valid = m0 < g.nmcu;
+  const int m = r.valid ? m0 : g.nmcu - 1;
+  r.my = m / g.mbw;
+  const int mx = m - r.my * g.mbw;
+  r.x = min(mx * mw + (j - ml * mw), fg.dw[pl ? 1 : 0] - 1);
+  r.img_off = pl == 0 ? j : kImgY + (pl - 1) * kImgC + j;
+  return r;
+}
+
+// Phase 1 of group grp: the wave's column tasks, each task's h entries loaded while the
+// previous task runs.
 template <int HT, int NPV, bool RANGE_ON>
 __device__ __forceinline__ void fused_scale_group(const uint8_t *frame, const EncGeom &g, const FusedGeom &fg,
-                                                  int grp, const uint32_t *htab0, const uint32_t *vtab0,
-                                                  const uint32_t *htab1, const uint32_t *vtab1, uint32_t *hbuf,
+                                                  int grp, const uint32_t *htab0, const uint32_t *htab1,
+                                                  const uint32_t *vtab0, const uint32_t *vtab1, uint32_t *hbuf,
                                                   uint8_t *img, int wave, int lane) {
+  int t = kFusedTasks[wave][0];
+  int pl = task_plane(t);
+  FusedTask tk = fused_task(g, fg, grp, t, pl, lane);
+  HCol<HT> hc = load_hcol<HT>(pl ? htab1 : htab0, tk.x);
 #pragma unroll 1
   for (int k = 0; k < 6; k++) {
-    const int t = kFusedTasks[wave][k];
-    if (t < 0) break;
-    const int pl = t < 8 ? 0 : (t < 12 ? 1 : 2);
-    const int j = (t < 8 ? t : (t & 3)) * 64 + lane;  // column within the group's plane strip
-    const int mw = pl ? 8 : 16;                         // MCU width in this plane
-    const int ml = j / mw, m = grp * kGroupMcus + ml;
-    const bool valid = m < g.nmcu;
-    const int mm = valid ? m : g.nmcu - 1;
-    const int my = mm / g.mbw, mx = mm - my * g.mbw;
-    const int pc = pl ? 1 : 0;
-    const int x = min(mx * mw + (j - ml * mw), fg.dw[pc] - 1);
-    uint8_t *dst = img + (pl == 0 ? j : kImgY + (pl - 1) * kImgC + j);
-    fused_column<HT, NPV, RANGE_ON>(frame, fg, pl, x, my * mw, mw, pl ? htab1 : htab0, pl ? vtab1 : vtab0,
-                                    hbuf, dst, pl ? 256 : 512, valid, lane, fg.npairs[pc]);
+    const int tn = kFusedTasks[wave][k + 1], pn = task_plane(tn);
+    FusedTask nk = tk;
+    HCol<HT> nc = hc;
+    if (tn >= 0) {  // prefetch the next task's h entry
+      nk = fused_task(g, fg, grp, tn, pn, lane);
+      nc = load_hcol<HT>(pn ? htab1 : htab0, nk.x);
+    }
+    fused_task_rows<HT, NPV, RANGE_ON>(frame, fg, pl, tk.my, hc, vtab0, vtab1, hbuf, img + tk.img_off, tk.valid,
+                                       lane);
+    if (tn < 0) break;
+    tk = nk;
+    hc = nc;
+    pl = pn;
   }
 }
 
@@ -226,15 +303,19 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
     // prologue: the DCs of the MCU before this unit's first group (the predecessors of chunk
     // 3 g0's first blocks), into s_dcx[parity of g0 - 1][2][2..7]
     if (g0 > 0) {
-      if (wave == 0 && lane < 32) {
+      const int m = g0 * kGroupMcus - 1, myp = m / g.mbw, mx = m - myp * g.mbw;
+      if (wave == 0 && lane < 32) {  // lanes 0-15: luma columns, 16-23: Cb, 24-31: Cr of MCU m
         const int pl = lane < 16 ? 0 : (lane < 24 ? 1 : 2);
-        const int m = g0 * kGroupMcus - 1, my = m / g.mbw, mx = m - my * g.mbw;
-        const int mw = pl ? 8 : 16, c = pl == 0 ? lane : (lane - 16) & 7;
-        const int pc = pl ? 1 : 0;
-        const int x = min(mx * mw + c, fg.dw[pc] - 1);
-        uint8_t *dst = img + (pl == 0 ? c : kImgY + (pl - 1) * kImgC + c);
-        fused_column<HT, NPV, RANGE_ON>(fr, fg, pl, x, my * mw, mw, pl ? htab1 : htab0, pl ? vtab1 : vtab0,
-                                        hbuf, dst, pl ? 256 : 512, true, lane, fg.npairs[pc]);
+        const int c = lane < 16 ? lane : (lane - 16) & 7;
+        const int x = min(mx * (pl ? 8 : 16) + c, fg.dw[pl ? 1 : 0] - 1);
+        const HCol<HT> hc = load_hcol<HT>(pl ? htab1 : htab0, x);
+        if (lane < 16)
+          fused_task_rows<HT, NPV, RANGE_ON>(fr, fg, 0, myp, hc, vtab0, vtab1, hbuf, img + c, true, lane);
+        else if (lane < 24)
+          fused_task_rows<HT, NPV, RANGE_ON>(fr, fg, 1, myp, hc, vtab0, vtab1, hbuf, img + kImgY + c, true, lane);
+        else
+          fused_task_rows<HT, NPV, RANGE_ON>(fr, fg, 2, myp, hc, vtab0, vtab1, hbuf, img + kImgY + kImgC + c,
+                                             true, lane);
       }
       __syncthreads();
       if (wave == 0 && lane < 6) {  // block `lane` of the MCU: 64-pixel sum -> quantised DC
@@ -250,7 +331,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
         }
         s_dcx[(g0 - 1) & 1][2][2 + lane] = (int)((sum + 32) >> 6);
       }
-      __syncthreads();  // the prologue's image is read before phase 1 overwrites it
+      __syncthreads();  // the prologue's image is done with
     }
     if (MODE == kCount && frame != aux_frame) {  // flush the previous frame's counts
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -266,7 +347,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
 
     for (int grp = g0; grp < g1; grp++) {
       // phase 1: the group's scaled pixels into the LDS image
-      fused_scale_group<HT, NPV, RANGE_ON>(fr, g, fg, grp, htab0, vtab0, htab1, vtab1, hbuf, img, wave, lane);
+      fused_scale_group<HT, NPV, RANGE_ON>(fr, g, fg, grp, htab0, htab1, vtab0, vtab1, hbuf, img, wave, lane);
       __syncthreads();
       // phase 2: chunk 3 grp + wave, lane = block
       const int chunk = grp * kFusedWaves + wave;

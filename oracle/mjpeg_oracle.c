@@ -587,7 +587,7 @@ typedef struct {
 static void or_huffman_compute_bits(or_ptable *prob_table, or_hufftable *distincts, int size,
                                     int max_length, int *ndistinct)
 {
-    static or_pm_list list_a, list_b;  /* large; the oracle is single-threaded per process */
+    or_pm_list list_a, list_b;  /* ~41 KB of stack: every call owns its lists (thread-safe) */
     or_pm_list *to = &list_a, *from = &list_b, *temp;
     int times, i = 0, j, k;
     int nbits[257] = { 0 };
@@ -805,7 +805,7 @@ size_t or_encode_planes_cfmt(const uint8_t *y, int ys, const uint8_t *u, int us,
     uint8_t obits[4][17], ovals[4][256];
     for (int t = 0; t < 4; t++) { bits[t] = or_default_bits[t]; vals[t] = or_default_vals[t]; }
     if (huff_optimal) {
-        static uint32_t counts[4][256];
+        uint32_t counts[4][256];
         int last_dc[3] = { 128, 128, 128 };
         memset(counts, 0, sizeof counts);
         for (size_t b = 0; b < nblocks; b++)

@@ -237,10 +237,12 @@ FUSED_CASES = [
     (1920, 1080, 1280, 720, 4, False, "smooth", 2, "default"),      # 1.5:1
     (1280, 720, 640, 360, 2, True, "patches", 3, "default"),
     (640, 360, 1280, 720, 5, False, "testsrc", 2, "default"),       # upscale: 4 taps
-    (400, 300, 200, 150, 6, False, "checker", 3, "optimal"),        # 13 MCUs per row: groups span rows
-    (96, 64, 48, 32, 3, True, "noise", 2, "default"),               # one partial group
-    (130, 98, 66, 50, 5, False, "smooth", 3, "default"),            # odd sizes, edge MCUs
+    (400, 300, 200, 150, 6, False, "checker", 3, "optimal"),        # < 32 MCUs per row: unfused
+    (96, 64, 48, 32, 3, True, "noise", 2, "default"),               # (unfused)
+    (1040, 530, 520, 265, 5, False, "smooth", 3, "default"),        # 33 MCUs per row, odd height
+    (1030, 520, 515, 260, 4, True, "checker", 2, "optimal"),        # edge MCU column, partial group
     (2200, 1300, 1100, 650, 7, False, "patches", 1, "default"),     # nmcu % 32 != 0
+    (1200, 700, 1023, 600, 3, False, "noise", 2, "default"),        # mild downscale
 ]
 
 

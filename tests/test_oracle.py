@@ -402,3 +402,19 @@ def test_tv_range_and_scale_for_422_444(chroma):
     got = np.asarray(im2.convert("YCbCr"))[..., 0].astype(float)
     ref = np.clip((y.astype(float) - 16) * 255 / 219, 0, 255)     # tv -> pc luma
     assert 10 * np.log10(255 ** 2 / np.mean((got - ref) ** 2)) > 30
+
+
+def test_oracle_is_thread_safe():
+    """The parity tests run the oracle on a thread pool (ctypes releases the GIL): concurrent
+    calls, -huffman optimal included, equal the serial results."""
+    from concurrent.futures import ThreadPoolExecutor
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420
+    from ffmpeg_distributed_amd.encoder import split_i420
+    w, h = 200, 120
+    frames = [split_i420(testsrc2_i420(w, h, t), w, h) for t in range(16)]
+    args = [dict(huffman="optimal", qscale=3), dict(huffman="default", qscale=5, dst_w=130, dst_h=70)]
+    for kw in args:
+        serial = [oracle.encode_frame(*f, **kw) for f in frames]
+        with ThreadPoolExecutor(8) as ex:
+            for _ in range(3):
+                assert list(ex.map(lambda f: oracle.encode_frame(*f, **kw), frames)) == serial

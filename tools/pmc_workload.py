@@ -15,6 +15,7 @@ def main():
     p.add_argument("--workload", default="c2")
     p.add_argument("--content", default="testsrc")
     p.add_argument("--launches", type=int, default=3)
+    p.add_argument("--unfused", action="store_true", help="-vf scale as k_scale + k_encode")
     a = p.parse_args()
     import torch
     import bench
@@ -29,7 +30,8 @@ def main():
         k = min(10, SEG - i)
         pool[i:i + k] = gen(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
-    enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF)
+    enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF,
+                       unfused=a.unfused)
     tot = 0
     for _ in range(a.launches):
         enc.submit(device_ptr=pool.data_ptr(), nframes=SEG)
