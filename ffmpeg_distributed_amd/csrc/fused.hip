@@ -42,7 +42,8 @@ constexpr int kFusedGroupsPerWg = 4;     // consecutive groups per workgroup
 constexpr int kFusedTabWords = 8;        // words per column (h) / row (v) filter entry
 constexpr int kImgY = 16 * 512, kImgC = 8 * 256;           // LDS image bytes per plane
 constexpr int kImgWords = (kImgY + 2 * kImgC) / 4;          // 3072
-constexpr int kHbufWords = kFusedWaves * kFusedMaxPairs * 64;  // 4032
+constexpr int kHbufWave = kFusedMaxPairs * 64 + 96;             // h-buffer + v-row table
+constexpr int kHbufWords = kFusedWaves * kHbufWave;
 constexpr int kPkWords = kFusedWaves * 32 * 64;                // 6144
 constexpr int kRegionWords = (kHbufWords + kImgWords) > kPkWords ? (kHbufWords + kImgWords) : kPkWords;
 
@@ -107,13 +108,34 @@ __device__ __forceinline__ HCol<HT> load_hcol(const uint32_t *__restrict__ htab,
 template <int HT, int NPV, int RANGE, int ROWS>
 __device__ __forceinline__ void fused_rows(const uint8_t *__restrict__ src, int sw, int sh, int dh, int my,
                                            const HCol<HT> &hc, const uint32_t *__restrict__ vtab,
-                                           uint32_t *hbuf, uint8_t *dst, int dpitch, bool valid, int lane,
-                                           int np) {
+                                           uint32_t *hbuf, uint32_t *s_vrow, uint8_t *dst, int dpitch, bool valid,
+                                           int lane, int np) {
   typedef uint64_t u64_unaligned __attribute__((aligned(1)));
   typedef uint32_t u32_unaligned __attribute__((aligned(1)));
   const int ybase = my * ROWS;
   const int ps0 = (int)vtab[(size_t)min(ybase, dh - 1) * kFusedTabWords];
   const int rmax = sh - 1;
+  // the task's v rows (ROWS x 6 words) into the wave's LDS row table: loaded now, stored after
+  // the h-pass (their latency hides behind it), read by the v-pass as uniform broadcasts
+  // (a partial wave -- the prologue, or one MCU row of a task that straddles two -- has its
+  // active lanes store the table first, each several entries)
+  constexpr int kVt = ROWS * 6, kVtPerLane = (kVt + 63) / 64;
+  const uint64_t act = __ballot(1);
+  const bool full = act == ~0ull;
+  uint32_t vtw[kVtPerLane];
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < kVtPerLane; k++) {
+      const int e = lane + 64 * k, row = e / 6, wd = e - row * 6;
+      vtw[k] = e < kVt ? vtab[(size_t)min(ybase + row, dh - 1) * kFusedTabWords + wd] : 0u;
+    }
+  } else {
+    const int na = __popcll(act), rk = __popcll(act & ((1ull << lane) - 1ull));
+    for (int e = rk; e < kVt; e += na) {
+      const int row = e / 6, wd = e - row * 6;
+      s_vrow[e] = vtab[(size_t)min(ybase + row, dh - 1) * kFusedTabWords + wd];
+    }
+  }
   const uint32_t hp = (uint32_t)hc.hpos;
   auto load = [&](uint64_t (&w)[2 * kFusedBatch], int p0) {
 #pragma unroll
@@ -145,11 +167,16 @@ __device__ __forceinline__ void fused_rows(const uint8_t *__restrict__ src, int 
     if (p0 + 2 * kFusedBatch < np) load(wa, p0 + 2 * kFusedBatch);
     compute(wb, p0 + kFusedBatch);
   }
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < kVtPerLane; k++)
+      if (lane + 64 * k < kVt) s_vrow[lane + 64 * k] = vtw[k];
+  }
   // v-pass: output row y reads the pairs [vps[y], vps[y] + NPV) against its pair coefficients
   const uint32_t *hcol = hbuf + lane;
 #pragma unroll 2
   for (int i = 0; i < ROWS; i++) {
-    const uint32_t *vr = vtab + (size_t)min(ybase + i, dh - 1) * kFusedTabWords;  // uniform
+    const uint32_t *vr = s_vrow + i * 6;  // uniform address: LDS broadcast
     const uint32_t *cp = hcol + ((int)vr[0] - ps0) * 64;
     int acc = 64 << 12;
 #pragma unroll
@@ -168,13 +195,14 @@ __device__ __forceinline__ void fused_task_rows(const uint8_t *frame, const Fuse
                                                 const HCol<HT> &hc, const uint32_t *vtab0, const uint32_t *vtab1,
                                                 uint32_t *hbuf, uint8_t *dst, bool valid, int lane) {
   const uint8_t *src = frame + fg.s_off[pl];
+  uint32_t *s_vrow = hbuf + kFusedMaxPairs * 64;  // the wave's v-row table (after its h-buffer)
   auto run = [&](int my_u) {
     if (pl == 0)
-      fused_rows<HT, NPV, RANGE_ON ? 1 : 0, 16>(src, fg.sw[0], fg.sh[0], fg.dh[0], my_u, hc, vtab0, hbuf, dst, 512,
-                                                 valid, lane, fg.npairs[0]);
+      fused_rows<HT, NPV, RANGE_ON ? 1 : 0, 16>(src, fg.sw[0], fg.sh[0], fg.dh[0], my_u, hc, vtab0, hbuf, s_vrow,
+                                                 dst, 512, valid, lane, fg.npairs[0]);
     else
-      fused_rows<HT, NPV, RANGE_ON ? 2 : 0, 8>(src, fg.sw[1], fg.sh[1], fg.dh[1], my_u, hc, vtab1, hbuf, dst, 256,
-                                                valid, lane, fg.npairs[1]);
+      fused_rows<HT, NPV, RANGE_ON ? 2 : 0, 8>(src, fg.sw[1], fg.sh[1], fg.dh[1], my_u, hc, vtab1, hbuf, s_vrow,
+                                                dst, 256, valid, lane, fg.npairs[1]);
   };
   const int my_a = __builtin_amdgcn_readfirstlane(my);
   if (my == my_a) run(my_a);
@@ -284,7 +312,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
   if (MODE == kCount)
     for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
 
-  uint32_t *hbuf = s_region + wave * kFusedMaxPairs * 64;
+  uint32_t *hbuf = s_region + wave * kHbufWave;
   uint8_t *img = (uint8_t *)(s_region + kHbufWords);
   uint32_t *s_pk = s_region + wave * 32 * 64;
   const int nblk = g.seg_blocks;
