@@ -29,8 +29,14 @@ def _command(out: str):
     # -fno-slp-vectorize: the SLP vectoriser packs k_encode's per-column fp32 chains into
     # v_pk_fma_f32 across columns, which doubles live registers (123 VGPRs -> 168 + 180 B
     # of scratch spills per lane) and costs ~30% of k_encode time.
+    # -dot6-insts / -dot4-insts: without the two-operand v_dot4c_i32_i8 / v_dot2c_i32_i16 forms the
+    # compiler emits the three-operand v_dot4_i32_i8 / v_dot2_i32_i16, which take the accumulator
+    # (or an SGPR) as a separate operand: no v_mov to copy a shared start value into every
+    # accumulator (k_scale_encode's h-pass: 2 per output).  The host compile ignores them.
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", out]
+           "-Xclang", "-target-feature", "-Xclang", "-dot6-insts",
+           "-Xclang", "-target-feature", "-Xclang", "-dot4-insts",
+           "-Wno-unused-command-line-argument", "-I", os.path.join(ROOT, "include"), "-o", out]
     return cmd + [os.path.join(CSRC, s) for s in SOURCES]
 
 

@@ -601,7 +601,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
           np = std::max(np, (int)c->ps[p].fv[(size_t)yb * kFusedTabWords] + sg.htaps / 2 + 1 -
                                 (int)c->ps[p].fv[(size_t)ya * kFusedTabWords]);
         }
-        np = (np + kFusedBatch - 1) / kFusedBatch * kFusedBatch;  // whole load batches (extra rows: clamped, unused)
+        np = (np + 1) & ~1;  // whole batches of 4 pairs plus a tail of 2 (extra rows: clamped, unused)
         fg.npairs[p] = np;
         if (np > kFusedMaxPairs) c->fused = false;
       }

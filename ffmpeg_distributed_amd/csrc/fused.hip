@@ -103,8 +103,7 @@ __device__ __forceinline__ HCol<HT> load_hcol(const uint32_t *__restrict__ htab,
 // rows, bytes to dst[i * dpitch] when `valid`.  Everything row-related is wave-uniform: the
 // source row addresses are scalar (the loads take the lane's tap position as their only
 // vector operand) and the v rows come by scalar loads.  The tap-window loads (np <=
-// kFusedMaxPairs row pairs, 8 B each, np a multiple of kFusedBatch) go out kFusedBatch pairs
-// ahead of their use.
+// kFusedMaxPairs row pairs, 8 B each, np even) go out kFusedBatch pairs ahead of their use.
 template <int HT, int NPV, int RANGE, int ROWS>
 __device__ __forceinline__ void fused_rows(const uint8_t *__restrict__ src, int sw, int sh, int dh, int my,
                                            const HCol<HT> &hc, const uint32_t *__restrict__ vtab,
@@ -157,15 +156,34 @@ __device__ __forceinline__ void fused_rows(const uint8_t *__restrict__ src, int 
   };
   // np is a multiple of kFusedBatch (host-rounded); the next batch's loads are issued before
   // the current batch is computed
+  // whole batches of kFusedBatch pairs, then a tail of 2 pairs when np % kFusedBatch == 2
+  const int nfull = np & ~(kFusedBatch - 1);
   uint64_t wa[2 * kFusedBatch], wb[2 * kFusedBatch];
-  load(wa, 0);
+  if (nfull) load(wa, 0);
 #pragma unroll 1
-  for (int p0 = 0; p0 < np; p0 += 2 * kFusedBatch) {
-    if (p0 + kFusedBatch < np) load(wb, p0 + kFusedBatch);
+  for (int p0 = 0; p0 < nfull; p0 += 2 * kFusedBatch) {
+    if (p0 + kFusedBatch < nfull) load(wb, p0 + kFusedBatch);
     compute(wa, p0);
-    if (p0 + kFusedBatch >= np) break;
-    if (p0 + 2 * kFusedBatch < np) load(wa, p0 + 2 * kFusedBatch);
+    if (p0 + kFusedBatch >= nfull) break;
+    if (p0 + 2 * kFusedBatch < nfull) load(wa, p0 + 2 * kFusedBatch);
     compute(wb, p0 + kFusedBatch);
+  }
+  if (np != nfull) {
+    uint64_t wt[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint8_t *row = src + (size_t)min(2 * (ps0 + nfull) + q, rmax) * sw;  // uniform
+      if constexpr (HT == 8)
+        wt[q] = *(const u64_unaligned *)(row + hp);
+      else
+        wt[q] = *(const u32_unaligned *)(row + hp);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int a = fused_hscale<HT, RANGE>(wt[2 * k], hc.c, hc.hs);
+      const int b = fused_hscale<HT, RANGE>(wt[2 * k + 1], hc.c, hc.hs);
+      hbuf[(nfull + k) * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
+    }
   }
   if (full) {
 #pragma unroll

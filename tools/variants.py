@@ -23,9 +23,9 @@ def parse():
 
 def build(name, src, flags):
     so = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
-           *flags, "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(src, "api.hip"),
-           os.path.join(CSRC, "sws_filter.cpp")]
+    from ffmpeg_distributed_amd import build as B  # the product's compile flags
+    base = [a for a in B._command(so) if not a.endswith((".hip", ".cpp"))]
+    cmd = base[:1] + [*flags] + base[1:] + [os.path.join(src, "api.hip"), os.path.join(CSRC, "sws_filter.cpp")]
     subprocess.run(cmd, check=True, cwd=src)
     return so
 
@@ -37,20 +37,23 @@ def main():
             build(*v)
         return
     import torch
+    import bench
     from ffmpeg_distributed_amd import _lib
     from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
-    W, H, N = 3840, 2160, 120
+    W, H, DW, DH, Q, N, FULL, HUFF, _ = bench.WORKLOADS[os.environ.get("WL", "c2")]
     dev = torch.device("cuda", 0)
-    pool = torch.empty((N, W * H * 3 // 2), dtype=torch.uint8, device=dev)
-    for i in range(0, N, 20):
-        pool[i:i + 20] = testsrc2_i420_torch(W, H, i, 20, dev)
+    pool = torch.empty((N, W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)), dtype=torch.uint8, device=dev)
+    for i in range(0, N, 10):
+        k = min(10, N - i)
+        pool[i:i + k] = testsrc2_i420_torch(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
     encs = {}
     for name, _, _ in vs:
         _lib._lib = None
         _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
         from ffmpeg_distributed_amd.encoder import MjpegEncoder
-        encs[name] = MjpegEncoder(0, W, H, qscale=5, max_batch=N, timing=True)
+        encs[name] = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, timing=True,
+                                  huffman=HUFF)
     res = {n: [] for n in encs}
     ref = None
     for rnd in range(6):
@@ -65,9 +68,9 @@ def main():
                 print(f"{n}: output {'==' if out == ref else '!='} first variant", flush=True)
             res[n].append(e.kernel_times()[0])
     for n, rows in res.items():
-        enc = sorted(r["encode"] for r in rows)
+        enc = sorted(r["encode"] + r["scale"] + r["huff"] for r in rows)
         tot = sorted(sum(r.values()) for r in rows)
-        print(f"{n:12s} k_encode median {enc[len(enc)//2]:.4f} ms (min {enc[0]:.4f}); "
+        print(f"{n:12s} scale+huff+encode median {enc[len(enc)//2]:.4f} ms (min {enc[0]:.4f}); "
               f"all kernels median {tot[len(tot)//2]:.4f} ms per {N} frames")
 
 
