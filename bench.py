@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=4.0,
                    help="CPU baseline: wall seconds per point of the core-count sweep")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--fused", action="store_true",
+                   help="-vf scale configs: the opt-in fused k_scale_encode instead of k_scale + k_encode")
     p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
     p.add_argument("--kernel-timing-detail", action="store_true",
                    help="events around every tail kernel too (adds ~10 us idle per event)")
@@ -265,7 +267,7 @@ def main():
 
     enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg,
                        timing=False if a.no_kernel_timing else ("detail" if a.kernel_timing_detail else True),
-                       huffman=HUFF, rst=a.rst)
+                       huffman=HUFF, rst=a.rst, fused=a.fused)
     bytes_out = []
 
     # Segments are pipelined two deep (mjg_submit queues up to two): segment s+1's kernels
@@ -298,7 +300,8 @@ def main():
     frames_total = a.steps * seg * world
     value = frames_total / dt
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
-    pmc = load_pmc(a.workload, a.content) if (seg == SEG and not a.rst and HUFF == WORKLOADS[a.workload][7]) else {}
+    pmc = load_pmc(a.workload, a.content) if (seg == SEG and not a.rst and not a.fused
+                                              and HUFF == WORKLOADS[a.workload][7]) else {}
     primary, per_kernel = rooflines(kt, seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H))
     primary = dict(primary, launches=nl)
 
@@ -331,7 +334,9 @@ def main():
                        "global_batch": seg * world, "parallelism": f"segment-dp{world}",
                        "profile": (f"-vf scale={DW}:{DH}:flags=bicubic " if (DW, DH) != (W, H) else "")
                        + f"-c:v mjpeg -q:v {Q} -dct int -huffman {HUFF} -bitexact"
-                       + (" -slices 8" if a.rst else "")},
+                       + (" -slices 8" if a.rst else ""),
+                       **({"scale_kernels": "k_scale_encode (fused)" if a.fused else "k_scale + k_encode"}
+                          if (DW, DH) != (W, H) else {})},
             "roofline": primary,
             "roofline_kernels": per_kernel,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},

@@ -581,9 +581,9 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     }
     // k_scale_encode: 4:2:0, one entropy-coded segment per frame (its 32-MCU groups are whole
     // chunks), filters it handles (HT 8 / 4 with D4 coefficients), row pairs within its
-    // h-buffer; otherwise k_scale + k_encode (MJG_F_UNFUSED asks for that path)
+    // h-buffer, and only when MJG_F_FUSED asks for it; otherwise k_scale + k_encode
     // (>= 32 MCUs per row: a group touches at most two MCU rows, whose v rows are staged in LDS)
-    c->fused = cf == MJG_CHROMA_420 && !c->rst && !(k.flags & (MJG_F_UNFUSED | MJG_F_DEBUG_COEFS)) &&
+    c->fused = cf == MJG_CHROMA_420 && !c->rst && (k.flags & MJG_F_FUSED) && !(k.flags & MJG_F_DEBUG_COEFS) &&
                c->ps[0].fusable && c->ps[1].fusable && c->ps[0].g.htaps == c->ps[1].g.htaps &&
                g.mbw >= kGroupMcus;
     if (c->fused) {
@@ -1047,7 +1047,7 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
 
 int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale, or scales fused (open it with MJG_F_UNFUSED)");
+  if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale, or scales fused (opened with MJG_F_FUSED)");
   if (c->nout > 0) {  // the scaled planes are shared by the slots: only the latest submit's
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;

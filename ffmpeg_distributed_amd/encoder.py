@@ -56,7 +56,7 @@ class MjpegEncoder:
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
                  debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
                  huffman: str = "default", chroma: str = "420", rst: bool = False,
-                 unfused: bool = False):
+                 fused: bool = False):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -80,8 +80,8 @@ class MjpegEncoder:
             raise ValueError(f"huffman {huffman!r}")
         if rst:
             flags |= _lib.MJG_F_RST
-        if unfused:  # -vf scale as k_scale + k_encode (scaled planes in HBM, debug_planes)
-            flags |= _lib.MJG_F_UNFUSED
+        if fused:  # -vf scale as one kernel, k_scale_encode (opt-in: slower on MI355X)
+            flags |= _lib.MJG_F_FUSED
         self.huffman = huffman
         self.chroma = str(chroma)
         if self.chroma not in _lib.CHROMA_FORMATS:

@@ -61,13 +61,15 @@ extern "C" {
 #define MJG_F_TIMING_DETAIL 64u /* MJG_F_TIMING plus events around every tail kernel (scan, 0xFF
                                   count, write: MJG_K_SCAN_BITS .. MJG_K_WRITE); each event adds
                                   ~10 us of GPU idle between those short kernels */
-#define MJG_F_UNFUSED 128u     /* with -vf scale: run the scale (k_scale, scaled frames to HBM) and
-                                  the encode as two kernels instead of the fused k_scale_encode
-                                  (which keeps the scaled pixels in LDS).  Same bytes; needed by
-                                  mjg_debug_planes.  MJG_F_DEBUG_COEFS implies it */
+#define MJG_F_FUSED 128u       /* with -vf scale: scale and encode in one kernel, k_scale_encode
+                                  (scaled pixels kept in LDS, never in HBM) instead of k_scale
+                                  (scaled frames to HBM) + k_encode.  Same bytes.  Opt-in: on
+                                  MI355X it measures slower than the two kernels (DESIGN.md
+                                  section 3b).  Ignored with MJG_F_DEBUG_COEFS, RST, non-4:2:0 or
+                                  filters it does not handle */
 
 /* Kernel ids for mjg_kernel_times() */
-#define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; unfused path only) */
+#define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */
 #define MJG_K_ENCODE 1         /* load [+ fused scale] + FDCT + quant + Huffman -> chunk bits */
 #define MJG_K_SCAN_BITS 2      /* per-frame exclusive scan of chunk bit lengths      */
 #define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk      */
@@ -158,7 +160,7 @@ int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, i
  * in coding order (4:2:0: Y0 Y1 Y2 Y3 Cb Cr per MCU).  Needs MJG_F_DEBUG_COEFS. */
 int mjg_debug_coefs(mjg_ctx *ctx, int frame, int16_t *out, size_t nblocks);
 /* The full-range encoder-input planes (after scale/range stage) of frame `frame`,
- * packed planar at dst size.  Only for a scaling config opened with MJG_F_UNFUSED. */
+ * packed planar at dst size.  Only for a scaling config on the k_scale path (not MJG_F_FUSED). */
 int mjg_debug_planes(mjg_ctx *ctx, int frame, uint8_t *out, size_t cap);
 /* Filter tables the context generated: plane 0 = luma, 1 = chroma; dir 0 = horizontal,
  * 1 = vertical.  taps/len may be queried with coeff == NULL. */

@@ -204,7 +204,7 @@ def test_scale_matches_oracle(sw, sh, dw, dh, full):
     kind = "testsrc" if sw >= 1000 else "smooth"
     frames = rand_frames(sw, sh, n, seed=11, kind=kind)
     q = 3
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, unfused=True) as enc:
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2) as enc:
         enc.submit(frames)
         enc.sync()
         planes = [enc.debug_planes(i) for i in range(n)]
@@ -225,7 +225,7 @@ def test_scale_matches_oracle(sw, sh, dw, dh, full):
         gy, gu, gv = split_i420(planes[i], dw, dh)
         assert (gy == ry).all() and (gu == ru).all() and (gv == rv).all()
     assert got == oracle_frames(frames, sw, sh, q, full, dw, dh)
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2) as enc:
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, fused=True) as enc:
         assert enc.encode(frames) == got  # the fused k_scale_encode path (where it applies)
 
 
@@ -251,10 +251,10 @@ def test_fused_scale_encode_matches_oracle(sw, sh, dw, dh, q, full, kind, n, huf
     """k_scale_encode (scaled pixels kept in LDS) byte-equal to the oracle's scale_plane +
     encode_frame, and to the unfused k_scale + k_encode path."""
     frames = rand_frames(sw, sh, n, seed=sw + dh + q, kind=kind)
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman) as enc:
-        got = enc.encode(frames)
     with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman,
-                      unfused=True) as enc:
+                      fused=True) as enc:
+        got = enc.encode(frames)
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman) as enc:
         got_unfused = enc.encode(frames)
     ref = _oracle_many(frames, sw, sh, dst_w=dw, dst_h=dh, full_range=full, qscale=q, huffman=huffman)
     for i in range(n):
@@ -262,9 +262,10 @@ def test_fused_scale_encode_matches_oracle(sw, sh, dw, dh, q, full, kind, n, huf
     assert got_unfused == got
 
 
-def test_fused_4k_segment_batch_from_device_memory():
+@pytest.mark.parametrize("fused", [False, True])
+def test_scaled_4k_segment_batch_from_device_memory(fused):
     """BASELINE configs[3] as bench.py submits it: 120 4K frames by device pointer through
-    the fused kernel, every frame equal to the oracle."""
+    k_scale + k_encode (and the opt-in fused kernel), every frame equal to the oracle."""
     import torch
     from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
     w, h, n = 3840, 2160, 120
@@ -274,7 +275,7 @@ def test_fused_4k_segment_batch_from_device_memory():
         pool[i:i + 20] = testsrc2_i420_torch(w, h, 500 + i, 20, dev)
     torch.cuda.synchronize()
     host = pool.cpu().numpy()
-    with MjpegEncoder(0, w, h, 1920, 1080, qscale=3, max_batch=n) as enc:
+    with MjpegEncoder(0, w, h, 1920, 1080, qscale=3, max_batch=n, fused=fused) as enc:
         enc.submit(device_ptr=pool.data_ptr(), nframes=n)
         got = enc.fetch()
     ref = _oracle_many(host, w, h, dst_w=1920, dst_h=1080, qscale=3)

@@ -15,9 +15,9 @@ from test_gpu_parity import rand_frames  # noqa: E402
 
 sw, sh, dw, dh, q, full, kind, n, huff = [eval(x) for x in sys.argv[1:10]]
 frames = rand_frames(sw, sh, n, seed=sw + dh + q, kind=kind)
-with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huff) as e:
+with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huff, fused=True) as e:
     got = e.encode(frames)
-with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huff, unfused=True) as e:
+with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huff) as e:  # k_scale + k_encode
     ref = e.encode(frames)
 for i in range(n):
     a = np.asarray(Image.open(io.BytesIO(got[i])).convert("YCbCr")).astype(int)

@@ -15,10 +15,10 @@ CASES = [(1040, 530, 520, 265), (1200, 700, 1023, 600), (3840, 2160, 1920, 1080)
 for sw, sh, dw, dh in CASES:
     frames = np.stack([testsrc2_i420(sw, sh, t) for t in range(2)])
     t0 = time.time()
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=3, max_batch=2, unfused=True) as e:
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=3, max_batch=2) as e:  # k_scale + k_encode
         ref = e.encode(frames)
     print(f"{sw}x{sh}->{dw}x{dh} unfused {time.time() - t0:.2f}s", flush=True)
     t0 = time.time()
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=3, max_batch=2) as e:
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=3, max_batch=2, fused=True) as e:
         got = e.encode(frames)
     print(f"{sw}x{sh}->{dw}x{dh} fused {time.time() - t0:.2f}s equal={got == ref}", flush=True)

@@ -15,7 +15,7 @@ def main():
     p.add_argument("--workload", default="c2")
     p.add_argument("--content", default="testsrc")
     p.add_argument("--launches", type=int, default=3)
-    p.add_argument("--unfused", action="store_true", help="-vf scale as k_scale + k_encode")
+    p.add_argument("--fused", action="store_true", help="-vf scale as the fused k_scale_encode")
     a = p.parse_args()
     import torch
     import bench
@@ -31,7 +31,7 @@ def main():
         pool[i:i + k] = gen(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
     enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF,
-                       unfused=a.unfused)
+                       fused=a.fused)
     tot = 0
     for _ in range(a.launches):
         enc.submit(device_ptr=pool.data_ptr(), nframes=SEG)
