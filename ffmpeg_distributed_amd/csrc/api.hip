@@ -343,7 +343,7 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   }
   for (int x0 = 0; x0 < dw; x0 += kScaleTileW) {  // same formula as k_scale's window
     const int xe = std::min(x0 + kScaleTileW, dw), cb = p.hf.pos[x0] & ~3;
-    max_nw = std::max(max_nw, ((p.hf.pos[xe - 1] + ht - cb + 3) >> 2) + 1);
+    max_nw = std::max(max_nw, ((((p.hf.pos[xe - 1] + ht - cb + 3) >> 2) + 1) + 3) & ~3);
   }
   ScaleGeom &g = p.g;
   g.htaps = ht;

@@ -6,8 +6,12 @@
 //   yuv2planeX_8_c: clip_u8(((64 << 12) + sum h*f) >> 19)  (12-bit coeffs, flat dither)
 //
 // One workgroup = a 64 x 32 output tile (4 waves, lane = output column).
-//   load:   the tile's source window (rows x dword-aligned columns) is staged in LDS with
-//           coalesced dword loads, many in flight per thread.
+//   load:   the tile's source window (rows x dword-aligned columns, rows padded to 16-byte
+//           pieces) is staged in LDS from 16-byte loads, 7 rows x 9 pieces per wave-instruction,
+//           all issued before any is waited on.  (Measured on MI355X, c4: a persistent
+//           variant that loads the next tile's window during this tile's passes ran ~20%
+//           slower -- tile index arithmetic, and 7 instead of 8 workgroups per CU -- and
+//           unaligned ds_read_b64 tap reads instead of the funnel shifts ran ~2x slower.)
 //   h-pass: wave w computes source row pairs p0+w, p0+w+4, ... of the window for its lane's
 //           column: taps funnel-shifted out of aligned LDS dwords (v_alignbit), widened to
 //           u16 pairs with v_perm and multiplied with v_dot2_i32_i16 against the column's
@@ -29,7 +33,9 @@ typedef short short2_t __attribute__((ext_vector_type(2)));
 
 constexpr int kScaleTileW = 64;
 constexpr int kScaleTileH = 32;
-constexpr int kScaleMaxRowsPerWave = 20;  // window rows per wave on the fast load path (2:1: 18)
+constexpr int kScaleLoadRows = 7, kScaleLoadsPerWave = 3;  // fast window path: 84 rows x 9 pieces
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
 
 struct ScaleGeom {
   int sw, sh, dw, dh;            // plane sizes
@@ -114,23 +120,36 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   // source window: dwords [cb, cb + nw) of rows [2 p0, 2 p1) (rows clamped to the plane;
   // the rows past it only meet zero coefficients), staged with coalesced dword loads
   const int cb = hp[x0] & ~3;
-  const int nw = ((hp[xe - 1] + g.htaps - cb + 3) >> 2) + 1;  // +1: the funnel shift reads one past
+  // +1: the funnel shift reads one past; rows padded to whole 16-byte pieces
+  const int nw = ((((hp[xe - 1] + g.htaps - cb + 3) >> 2) + 1) + 3) & ~3;
   uint32_t *win = smem;                                       // [nrows][nw]
   uint32_t *pairs = smem + g.lds_win_words;                   // [p1 - p0][64]
   uint32_t *vtab = pairs + g.lds_pairs * kScaleTileW;         // [ye - y0][1 + npv]: pair start, coefficients
-  const bool fast = nw <= 64 && nrows <= 4 * kScaleMaxRowsPerWave && g.sw >= 4;
+  const bool fast = nw <= 36 && nrows <= 4 * kScaleLoadsPerWave * kScaleLoadRows && g.sw >= 16;
   // Every global load of the tile is issued before any is waited on: the window rows, this
   // lane's h filter (column x), and the tile's v filter rows (one entry per thread).
-  uint32_t v[kScaleMaxRowsPerWave];
-  const int col = cb + 4 * lane, lcol = min(col, max(g.sw - 4, 0));
-  const uint32_t drop = (uint32_t)(col - lcol) * 8;
+  // fast path: 16-byte pieces, 7 rows of 9 pieces per wave-instruction, 3 per wave (84 rows
+  // of <= 144 bytes)
+  u32x4 v[kScaleLoadsPerWave];
+  const int rr = lane / 9, pc = lane - 9 * rr, col = cb + 16 * pc;
   if (fast) {
-    // wave per row, lane per dword.  A dword crossing the row end is loaded from sw-4 and
-    // shifted down (bytes >= sw are never used).
-    const uint8_t *sc = s + lcol;
 #pragma unroll
-    for (int j = 0; j < kScaleMaxRowsPerWave; j++)  // unconditional: every address is in-plane
-      v[j] = *(const u32_unaligned *)(sc + (size_t)min(2 * p0 + wave + 4 * j, g.sh - 1) * g.s_stride);
+    for (int i = 0; i < kScaleLoadsPerWave; i++) {
+      const int r = kScaleLoadRows * (kScaleLoadsPerWave * wave + i) + rr;
+      const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
+      if (col + 16 <= g.sw) {
+        v[i] = *(const u32x4_a4 *)(rp + col);
+      } else {  // the piece crosses the row end: dwords loaded in-row and shifted down (bytes
+                // >= sw meet no tap)
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int cc = col + 4 * k, lc = min(cc, g.sw - 4);
+          w[k] = cc < g.sw ? *(const u32_unaligned *)(rp + lc) >> ((cc - lc) * 8) : 0u;
+        }
+        v[i] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    }
   }
   const int x = min(x0 + lane, g.dw - 1);  // clamped: tail lanes redo the last column
   const int32_t *hc = hcp + (size_t)x * (g.htaps >> 1);
@@ -148,9 +167,10 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   }
   if (fast) {
 #pragma unroll
-    for (int j = 0; j < kScaleMaxRowsPerWave; j++) {
-      const int r = wave + 4 * j;
-      if (r < nrows && lane < nw) win[r * nw + lane] = (v[j] >> drop) ^ (D4 ? 0x80808080u : 0u);
+    for (int i = 0; i < kScaleLoadsPerWave; i++) {
+      const int r = kScaleLoadRows * (kScaleLoadsPerWave * wave + i) + rr;
+      const u32x4 w = D4 ? v[i] ^ 0x80808080u : v[i];
+      if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw) *(u32x4 *)(win + r * nw + 4 * pc) = w;
     }
   } else {
     for (int i = tid; i < nrows * nw; i += 256) {
@@ -163,6 +183,7 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
       win[i] = w ^ (D4 ? 0x80808080u : 0u);
     }
   }
+#pragma unroll 1
   for (; vi < nvt; vi += 256) {  // (one pass unless npv > 7)
     if (vi != tid) {
       const int yy = vi / (npv + 1), k = vi - yy * (npv + 1);
