@@ -37,7 +37,7 @@ MJG_NUM_KERNELS = len(KERNEL_NAMES)
 
 # Every symbol include/mjgpu.h declares (checked by tests/test_abi.py).
 EXPORTS = (
-    "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_open", "mjg_close",
+    "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_device_numa_node", "mjg_open", "mjg_close",
     "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch",
     "mjg_output_device", "mjg_stream", "mjg_host_alloc", "mjg_host_free",
     "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
@@ -79,6 +79,8 @@ def load():
         L.mjg_version.restype = C.c_int
         L.mjg_last_error.restype = C.c_char_p
         L.mjg_device_count.restype = C.c_int
+        L.mjg_device_numa_node.argtypes = [C.c_int]
+        L.mjg_device_numa_node.restype = C.c_int
         L.mjg_open.argtypes = [C.c_int, C.POINTER(MjgConfig), C.POINTER(vp)]
         L.mjg_close.argtypes = [vp]
         L.mjg_close.restype = None
@@ -116,6 +118,11 @@ def check(rc: int) -> int:
 
 def device_count() -> int:
     return check(load().mjg_device_count())
+
+
+def device_numa_node(device: int) -> int:
+    """NUMA node of the device (-1: unknown)."""
+    return check(load().mjg_device_numa_node(int(device)))
 
 
 def build_header(dst_w: int, dst_h: int, qscale: int, sar=(1, 1), com_itu601: bool = False,

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -723,6 +724,20 @@ int mjg_device_count(void) {
   int n = 0;
   HIP_TRY(hipGetDeviceCount(&n));
   return n;
+}
+
+int mjg_device_numa_node(int device) {
+  char bus[64] = {0};
+  HIP_TRY(hipDeviceGetPCIBusId(bus, (int)sizeof bus, device));
+  for (char *p = bus; *p; p++) *p = (char)tolower((unsigned char)*p);
+  char path[160];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  return node < 0 ? -1 : node;
 }
 
 int mjg_open(int device, const mjg_config *cfg, mjg_ctx **out) {

@@ -84,6 +84,107 @@ class Progress:
 
 
 READ_THREADS = int(os.environ.get("MJG_READ_THREADS", "4"))
+# MJG_WORKER_TRACE=1: one `mjg-trace:` stderr line per segment with where its time went
+# (reader, submit, sync, fetch, mux) and the process's CPU / NUMA placement.
+TRACE = os.environ.get("MJG_WORKER_TRACE", "0") == "1"
+# Bind the worker to its GPU's NUMA node (CPUs, and preferred memory for its page-locked
+# batches), see bind_numa.  MJG_NUMA_BIND=0 leaves placement to the scheduler.
+NUMA_BIND = os.environ.get("MJG_NUMA_BIND", "1") == "1"
+_bound_node: Optional[int] = None
+_gpu_node = -1
+
+
+def bind_numa(device: int) -> int:
+    """Run this process's threads from here on on the CPUs of `device`'s NUMA node and
+    prefer that node for its memory: the segment's positional reads copy page-cache pages
+    into page-locked batches that the GPU then reads over PCIe, and both the copy and the
+    DMA cross the socket interconnect when the process sits on the other node.  Threads
+    started later (reader, pread pool) inherit the mask; the process's first allocation of
+    the batches follows the memory policy.  Returns the node (-1: unknown / not bound)."""
+    global _bound_node, _gpu_node
+    if _bound_node is not None:
+        return _bound_node
+    _bound_node = -1
+    from . import _lib
+    try:
+        node = _gpu_node = _lib.device_numa_node(device)
+    except Exception:
+        return -1
+    if node < 0 or not NUMA_BIND:
+        return -1
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = _cpulist(f.read().strip()) & os.sched_getaffinity(0)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+    except OSError:
+        return -1
+    _prefer_node(node)
+    _bound_node = node
+    return node
+
+
+def _prefer_node(node: int) -> None:
+    """set_mempolicy(MPOL_PREFERRED, {node}) for the calling thread (x86-64 Linux)."""
+    import ctypes
+    import platform
+    if platform.machine() != "x86_64" or node >= 64:
+        return
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        mask = ctypes.c_ulong(1 << node)
+        libc.syscall(238, 1, ctypes.byref(mask), ctypes.c_ulong(64))  # SYS_set_mempolicy
+    except (OSError, AttributeError):
+        pass
+
+
+def placement() -> str:
+    """CPUs this process may run on, the NUMA nodes they span and the cgroup's CPU
+    throttling counters (tracing only; Linux /proc and /sys, best effort)."""
+    out = []
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        out.append(f"cpus={len(cpus)}")
+        nodes = {}
+        base = "/sys/devices/system/node"
+        for d in os.listdir(base):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(f"{base}/{d}/cpulist") as f:
+                    lst = _cpulist(f.read().strip())
+                k = len(lst & set(cpus))
+                if k:
+                    nodes[int(d[4:])] = k
+        out.append("nodes=" + ",".join(f"{n}:{k}" for n, k in sorted(nodes.items())))
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            st = dict(line.split() for line in f if line.strip())
+        out.append(f"throttled={st.get('nr_throttled', '?')}/{st.get('nr_periods', '?')}"
+                   f" throttled_ms={int(st.get('throttled_usec', 0)) // 1000}")
+    except (OSError, ValueError):
+        pass
+    out.append(f"cpu_now={_current_cpu()} gpu_node={_gpu_node} bound={_bound_node}")
+    return " ".join(out)
+
+
+def _cpulist(text: str) -> set:
+    cpus = set()
+    for part in text.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def _current_cpu() -> int:
+    try:
+        with open("/proc/thread-self/stat") as f:
+            return int(f.read().rsplit(")", 1)[1].split()[36])
+    except (OSError, ValueError, IndexError):
+        return -1
 
 
 def _regular_file_fd(f) -> Optional[int]:
@@ -283,6 +384,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         stderr.flush()
         return ffmpeg_fallthrough(src, args, stdout)
     dst_w, dst_h = prof.scale or (info.width, info.height)
+    bind_numa(device)  # before the reader threads and the batch buffers
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
     batch = BATCH or max(1, min(32, BATCH_BYTES // max(info.frame_bytes, 1)))
@@ -317,13 +419,18 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     for i in range(nbuf):
         free.put(i)
 
+    tr = {"read": 0.0, "submit": 0.0, "sync": 0.0, "fetch": 0.0, "mux": 0.0, "wait": 0.0}
+    t_seg = time.monotonic()
+
     def reader():
         try:
             while True:
                 i = free.get()
                 if i < 0 or abort.is_set():
                     return
+                t0 = time.monotonic()
                 n = src.read_into(bufs[i].array, batch)
+                tr["read"] += time.monotonic() - t0
                 full.put((i, n))
                 if n < batch:
                     full.put(None)
@@ -339,18 +446,26 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     def drain_one():
         nonlocal frames
         j, m = queued.pop(0)
+        t0 = time.monotonic()
         enc.sync()
+        t1 = time.monotonic()
         packets = enc.fetch()
+        t2 = time.monotonic()
         free.put(j)
         for p in packets:
             mkv.write_frame(p)
+        tr["sync"] += t1 - t0
+        tr["fetch"] += t2 - t1
+        tr["mux"] += time.monotonic() - t2
         frames += m
         prog.update(frames, sum(len(p) for p in packets))
 
     failed = True
     try:
         while True:
+            t0 = time.monotonic()
             item = full.get()
+            tr["wait"] += time.monotonic() - t0
             if item is None:
                 break
             if isinstance(item, BaseException):
@@ -359,7 +474,9 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
             if n:
                 if len(queued) == 2:
                     drain_one()
+                t0 = time.monotonic()
                 enc.submit(bufs[i].array[: n * fb], n)
+                tr["submit"] += time.monotonic() - t0
                 queued.append((i, n))
             else:
                 free.put(i)
@@ -368,6 +485,10 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         mkv.close()
         prog.update(frames, 0, final=True)
         failed = False
+        if TRACE:
+            stderr.write(f"mjg-trace: frames={frames} total={time.monotonic() - t_seg:.4f} "
+                         + " ".join(f"{k}={v:.4f}" for k, v in tr.items()) + f" {placement()}\n")
+            stderr.flush()
     finally:
         # Nothing is freed while a reader could still write into a batch buffer: stop the
         # reader thread (it finishes at most the read in flight, whose positional reads it

@@ -98,6 +98,9 @@ int mjg_version(void);
 const char *mjg_last_error(void);
 /* Number of visible HIP devices, or a negative MJG_E_* code. */
 int mjg_device_count(void);
+/* NUMA node of `device` (its PCI function's numa_node in sysfs), -1 when the platform does
+ * not say, or a negative MJG_E_* code.  The worker binds its reader threads to that node. */
+int mjg_device_numa_node(int device);
 
 /* Create a context on `device`: validates cfg, builds quant/Huffman/filter tables,
  * allocates device buffers for cfg->max_batch frames.  Replaces one

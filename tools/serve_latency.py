@@ -1,7 +1,11 @@
-"""Per-segment time of `worker --serve` (tool): requests one at a time (the dispatcher's
-pattern) vs all at once, and in-process serve() for comparison.
-    python tools/serve_latency.py c1d 250 5"""
-import io
+"""Per-segment time of `worker --serve` (tool), and where it goes: P server processes are
+started one after another; each encodes R copies of one segment, requests sent one at a
+time (the dispatcher's pattern).  Workers run with MJG_WORKER_TRACE=1, so every segment
+also reports its reader / submit / sync / fetch / mux seconds and the process's CPU and
+NUMA placement (and the GPU's NUMA node); MJG_NUMA_BIND=0 turns the worker's binding off.
+    python tools/serve_latency.py c1d 250 --servers 6 --reps 4 [--no-bind]"""
+import argparse
+import json
 import os
 import subprocess
 import sys
@@ -13,47 +17,42 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import e2e_worker as E  # noqa: E402
 
-wl, frames, reps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-w, h, fps, args = E.WORKLOADS[wl]
-d = tempfile.mkdtemp()
+ap = argparse.ArgumentParser()
+ap.add_argument("workload")
+ap.add_argument("frames", type=int)
+ap.add_argument("--servers", type=int, default=4)
+ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--no-bind", action="store_true")
+ap.add_argument("--dir", default=None)
+a = ap.parse_args()
+w, h, fps, args = E.WORKLOADS[a.workload]
+d = tempfile.mkdtemp(dir=a.dir)
 seg = os.path.join(d, "seg.mkv")
-E.make_segment(seg, w, h, fps, frames, full_range=wl in E.FULL_RANGE)
+E.make_segment(seg, w, h, fps, a.frames, full_range=a.workload in E.FULL_RANGE)
 argv = [sys.executable, "-m", "ffmpeg_distributed_amd.worker", "--device", "0", *args, "--serve"]
+env = dict(os.environ, MJG_WORKER_TRACE="1", MJG_NUMA_BIND="0" if a.no_bind else "1")
 
-
-def done_lines(p, k):
-    t = []
-    for line in p.stderr:
-        if line.startswith("mjg-serve: segment done"):
-            t.append(time.monotonic())
-            if len(t) == k:
-                return t
-    raise SystemExit("server exited")
-
-
-p = subprocess.Popen(argv, stdin=subprocess.PIPE, stderr=subprocess.PIPE, stdout=subprocess.DEVNULL,
-                     universal_newlines=True, bufsize=1, cwd=ROOT)
-one = []
-for i in range(reps):
-    t0 = time.monotonic()
-    p.stdin.write(f"{seg}\t{d}/o{i}.mkv\n")
-    p.stdin.flush()
-    one.append(done_lines(p, 1)[0] - t0)
-t0 = time.monotonic()
-p.stdin.write("".join(f"{seg}\t{d}/p{i}.mkv\n" for i in range(reps)))
-p.stdin.flush()
-ts = done_lines(p, reps)
-allat = [b - a for a, b in zip([t0] + ts[:-1], ts)]
-p.stdin.close()
-p.wait()
-from ffmpeg_distributed_amd import worker  # noqa: E402
-err = io.StringIO()
-t0 = time.monotonic()
-worker.serve(0, args, requests=io.StringIO("".join(f"{seg}\t{d}/q{i}.mkv\n" for i in range(reps))), stderr=err)
-inproc = time.monotonic() - t0
-print(wl, frames, "one-at-a-time", [round(x, 3) for x in one])
-print(wl, frames, "all-at-once", [round(x, 3) for x in allat])
-print(wl, frames, "in-process total incl. init", round(inproc, 3))
+for s in range(a.servers):
+    p = subprocess.Popen(argv, stdin=subprocess.PIPE, stderr=subprocess.PIPE, stdout=subprocess.DEVNULL,
+                         universal_newlines=True, bufsize=1, cwd=ROOT, env=env)
+    times, traces = [], []
+    for i in range(a.reps):
+        t0 = time.monotonic()
+        p.stdin.write(json.dumps([seg, f"{d}/o{s}_{i}.mkv"]) + "\n")
+        p.stdin.flush()
+        for line in p.stderr:
+            if line.startswith("mjg-trace:"):
+                traces.append(line.split(":", 1)[1].strip())
+            if line.startswith("mjg-serve: segment done"):
+                times.append(round(time.monotonic() - t0, 4))
+                break
+        else:
+            raise SystemExit("server exited")
+    p.stdin.close()
+    p.wait()
+    print(f"{a.workload} {a.frames} server {s} bind={not a.no_bind} seconds {times}", flush=True)
+    for t in traces[1:]:
+        print("   ", t, flush=True)
 for f in os.listdir(d):
     os.remove(os.path.join(d, f))
 os.rmdir(d)
