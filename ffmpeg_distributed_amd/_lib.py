@@ -38,7 +38,7 @@ MJG_NUM_KERNELS = len(KERNEL_NAMES)
 # Every symbol include/mjgpu.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_device_numa_node", "mjg_open", "mjg_close",
-    "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch",
+    "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch", "mjg_fetch_host",
     "mjg_output_device", "mjg_stream", "mjg_host_alloc", "mjg_host_free",
     "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
     "mjg_debug_planes", "mjg_debug_filter",
@@ -90,6 +90,7 @@ def load():
         L.mjg_submit.argtypes = [vp, vp, C.c_int, C.c_int]
         L.mjg_sync.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.mjg_fetch.argtypes = [vp, vp, sz]
+        L.mjg_fetch_host.argtypes = [vp, C.POINTER(vp), C.POINTER(sz)]
         L.mjg_output_device.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
         L.mjg_stream.argtypes = [vp]
         L.mjg_stream.restype = vp

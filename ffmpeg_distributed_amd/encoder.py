@@ -175,12 +175,13 @@ class MjpegEncoder:
         if self._queued and not self._synced_since_submit:
             self.sync()
         sizes = self._last_sizes
-        total = int(sizes.sum())
-        buf = np.empty(max(total, 1), np.uint8)
-        check(self._L.mjg_fetch(self._h, C.c_void_p(buf.ctypes.data), buf.size))
-        out, o = [], 0
+        data, n = C.c_void_p(), C.c_size_t()
+        check(self._L.mjg_fetch_host(self._h, C.byref(data), C.byref(n)))  # page-locked copy
+        if int(n.value) != int(sizes.sum()):
+            raise MjgError(_lib.MJG_E_STATE, "fetch size mismatch")
+        out, o = [], int(data.value or 0)
         for s in sizes:
-            out.append(buf[o: o + int(s)].tobytes())
+            out.append(C.string_at(o, int(s)))
             o += int(s)
         return out
 

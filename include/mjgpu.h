@@ -133,6 +133,10 @@ int mjg_sync(mjg_ctx *ctx, uint64_t *frame_sizes, uint64_t *total);
 /* Copy the packed JPEGs of the last synced submit (frame after frame) to host memory; syncs
  * the oldest queued submit first when mjg_sync was not called since the last mjg_submit. */
 int mjg_fetch(mjg_ctx *ctx, uint8_t *out, size_t cap);
+/* The same bytes without the copy into caller memory: *data points at the context's
+ * page-locked copy (DMA'd from the device), *len its size; valid until the next
+ * mjg_fetch / mjg_fetch_host or mjg_close. */
+int mjg_fetch_host(mjg_ctx *ctx, const uint8_t **data, size_t *len);
 /* Device pointers of the packed output and of the per-frame byte offsets (nframes+1
  * entries, valid after mjg_sync). */
 int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offsets);
