@@ -505,13 +505,24 @@ class MkvWriter:
             self._flush()
         if not self._cluster:
             self._cluster_ts = ts
+            self._cluster_bytes = 0
         rel = ts - self._cluster_ts
-        self._cluster.append(element(SIMPLE_BLOCK, b"\x81" + struct.pack(">hB", rel, 0x80) + jpeg))
+        # the SimpleBlock's header (ID, size, track 1, timecode, keyframe flag); the JPEG is
+        # written after it as its own piece: no per-frame copy of the payload
+        body = 4 + len(jpeg)
+        head = _id_bytes(SIMPLE_BLOCK) + _size_bytes(body) + b"\x81" + struct.pack(">hB", rel, 0x80)
+        self._cluster.append((head, jpeg))
+        self._cluster_bytes += len(head) + len(jpeg)
         self.n += 1
 
     def _flush(self):
         if self._cluster:
-            self.f.write(element(CLUSTER, uint_el(TIMESTAMP, self._cluster_ts) + b"".join(self._cluster)))
+            ts = uint_el(TIMESTAMP, self._cluster_ts)
+            pieces = [_id_bytes(CLUSTER) + _size_bytes(len(ts) + self._cluster_bytes) + ts]
+            for head, jpeg in self._cluster:
+                pieces.append(head)
+                pieces.append(jpeg)
+            self.f.writelines(pieces)
             self._cluster = []
 
     def close(self):

@@ -37,6 +37,9 @@ DECODE_ARGV = ["ffmpeg", "-v", "error", "-f", "matroska", "-i", "pipe:", "-map",
 # large part of its start-up: 4K batches of 32 frames pinned 1.2 GB, of 8 frames 0.3 GB.
 BATCH = int(os.environ.get("MJG_WORKER_BATCH", "0"))
 BATCH_BYTES = int(os.environ.get("MJG_WORKER_BATCH_BYTES", str(96 << 20)))
+# serve mode pins its batches once for many segments: larger batches (an 8K batch of 1 frame
+# leaves the GPU waiting on every sync)
+SERVE_BATCH_BYTES = int(os.environ.get("MJG_SERVE_BATCH_BYTES", str(256 << 20)))
 # FFmpeg builds differ in the pix_fmt their CLI hands the mjpeg encoder for yuv420p input
 # (yuvj420p: no COM; yuv420p + full range: COM "CS=ITU601"); default = yuvj420p.
 COM_ITU601 = os.environ.get("MJG_COM_ITU601", "0") == "1"
@@ -364,7 +367,8 @@ def ffmpeg_fallthrough(src: Source, args: List[str], stdout) -> int:
     return rc or src.close()
 
 
-def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cache=None) -> int:
+def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cache=None,
+        batch_bytes: Optional[int] = None) -> int:
     """One segment, stdin -> stdout.  `cache` (serve mode): a dict that keeps the encoder
     context and the page-locked batch buffers between segments of the same stream shape."""
     stdin = stdin or sys.stdin.buffer
@@ -387,7 +391,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     bind_numa(device)  # before the reader threads and the batch buffers
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
-    batch = BATCH or max(1, min(32, BATCH_BYTES // max(info.frame_bytes, 1)))
+    batch = BATCH or max(1, min(32, (batch_bytes or BATCH_BYTES) // max(info.frame_bytes, 1)))
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     key = (info.width, info.height, dst_w, dst_h, info.full_range, prof.qscale, sar,
@@ -442,23 +446,45 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     th.start()
     frames = 0
     queued: "list" = []  # buffer index and frame count per submit, oldest first
+    # the muxer thread writes each synced submit's packets while the main thread keeps the
+    # GPU fed (a 4K segment's 120 JPEGs are ~20 MB of writes)
+    outq: "queue.Queue" = queue.Queue(maxsize=4)
+    mux_err: list = []
+
+    def muxer():
+        nonlocal frames
+        while True:
+            item = outq.get()
+            if item is None:
+                return
+            if mux_err:
+                continue  # drain after a failure
+            packets, m = item
+            try:
+                t0 = time.monotonic()
+                for p in packets:
+                    mkv.write_frame(p)
+                tr["mux"] += time.monotonic() - t0
+                frames += m
+                prog.update(frames, sum(len(p) for p in packets))
+            except BaseException as e:  # surfaced by the main thread
+                mux_err.append(e)
+
+    mt = threading.Thread(target=muxer, daemon=True)
+    mt.start()
 
     def drain_one():
-        nonlocal frames
         j, m = queued.pop(0)
         t0 = time.monotonic()
         enc.sync()
         t1 = time.monotonic()
         packets = enc.fetch()
-        t2 = time.monotonic()
-        free.put(j)
-        for p in packets:
-            mkv.write_frame(p)
         tr["sync"] += t1 - t0
-        tr["fetch"] += t2 - t1
-        tr["mux"] += time.monotonic() - t2
-        frames += m
-        prog.update(frames, sum(len(p) for p in packets))
+        tr["fetch"] += time.monotonic() - t1
+        free.put(j)
+        if mux_err:
+            raise mux_err[0]
+        outq.put((packets, m))
 
     failed = True
     try:
@@ -482,6 +508,10 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
                 free.put(i)
         while queued:
             drain_one()
+        outq.put(None)
+        mt.join()
+        if mux_err:
+            raise mux_err[0]
         mkv.close()
         prog.update(frames, 0, final=True)
         failed = False
@@ -496,6 +526,9 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         # the source, and only then the encoder and the page-locked buffers.
         abort.set()
         free.put(-1)
+        if mt.is_alive():  # error path: let the muxer finish what it holds, then stop
+            outq.put(None)
+            mt.join(timeout=5.0)
         th.join(timeout=5.0)
         if th.is_alive():
             src.close(kill=True)
@@ -549,7 +582,8 @@ def serve(device: int, args: List[str], requests=None, stderr=None) -> int:
             try:
                 src, dst = json.loads(line)
                 with open(src, "rb") as fin, open(dst, "wb") as fout:
-                    rc = run(device, args, stdin=fin, stdout=fout, stderr=stderr, cache=cache)
+                    rc = run(device, args, stdin=fin, stdout=fout, stderr=stderr, cache=cache,
+                             batch_bytes=SERVE_BATCH_BYTES)
             except Exception as e:
                 stderr.write(f"gpu:{device}: {type(e).__name__}: {e}\n")
                 rc = 1

@@ -177,7 +177,7 @@ def test_worker_serve_protocol(tmp_path, monkeypatch):
     from ffmpeg_distributed_amd import worker
     calls = []
 
-    def fake_run(dev, args, stdin, stdout, stderr, cache):
+    def fake_run(dev, args, stdin, stdout, stderr, cache, batch_bytes=None):
         data = stdin.read()
         calls.append((dev, args, data, id(cache)))
         if data == b"boom":
@@ -206,7 +206,7 @@ def test_serve_request_survives_any_path(tmp_path, monkeypatch):
     from ffmpeg_distributed_amd import dispatcher as D, worker
     seen = []
 
-    def fake_run(dev, args, stdin, stdout, stderr, cache):
+    def fake_run(dev, args, stdin, stdout, stderr, cache, batch_bytes=None):
         seen.append(stdin.read())
         stdout.write(b"ok")
         return 0

@@ -106,7 +106,7 @@ def main():
         pers = []
         for i in range(a.persistent):
             t = time.monotonic()
-            p.stdin.write(f"{seg}\t{os.path.join(d, f'pers{i}.mkv')}\n")
+            p.stdin.write(json.dumps([seg, os.path.join(d, f"pers{i}.mkv")]) + "\n")
             p.stdin.flush()
             for line in p.stderr:
                 if line.startswith("mjg-serve: segment done rc="):
