@@ -212,8 +212,18 @@ class MkvReader:
         self._in_track: Optional[MkvTrack] = None
         self._eof = False
         self.duration: Optional[float] = None     # Info/Duration, timescale units
-        while not self.tracks or self._in_track is not None:
-            if not self._step():
+        # headers up to the first Cluster's start (its blocks are left to the frame readers:
+        # an 8K block is 50 MB, not something to read -- and record -- while parsing headers)
+        while True:
+            eid, _ = _read_vint(self.f, True)
+            if eid is None:
+                self._eof = True
+                break
+            size, _ = _read_vint(self.f, False)
+            if eid == CLUSTER and self.tracks:
+                self._in_track = None
+                break
+            if not self._element(eid, size) or (self.tracks and self._in_track is None and self._pending):
                 break
 
     def _step(self) -> bool:

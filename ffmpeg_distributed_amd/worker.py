@@ -371,6 +371,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         batch_bytes: Optional[int] = None) -> int:
     """One segment, stdin -> stdout.  `cache` (serve mode): a dict that keeps the encoder
     context and the page-locked batch buffers between segments of the same stream shape."""
+    t_run = time.monotonic()
     stdin = stdin or sys.stdin.buffer
     stdout = stdout or sys.stdout.buffer
     stderr = stderr or sys.stderr
@@ -517,6 +518,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         failed = False
         if TRACE:
             stderr.write(f"mjg-trace: frames={frames} total={time.monotonic() - t_seg:.4f} "
+                         f"setup={t_seg - t_run:.4f} "
                          + " ".join(f"{k}={v:.4f}" for k, v in tr.items()) + f" {placement()}\n")
             stderr.flush()
     finally:
