@@ -20,7 +20,7 @@ from pmc_summary import load, load_totals  # noqa: E402
 KERNEL_WIDTH = {
     "k_encode": (8, 4),       # 8-byte pixel row loads, slot words
     "k_fused": (4, 4),        # 4-byte window loads (scale + encode), slot words
-    "k_scale": (4, 1),        # dword window loads, one output byte per lane
+    "k_scale": (8, 1),        # 16-byte window loads (4 and 8 B reads calibrate alike), byte stores
     "k_emit_syms": (4, 4),    # symbol record words, slot words
     "k_count_ff": (4, 4),     # slot words
     "k_write": (4, 1),        # slot words in, stuffed bytes out
