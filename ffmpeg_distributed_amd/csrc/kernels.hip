@@ -211,6 +211,7 @@ struct ShiftSink {
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   uint32_t bits = 0;
   uint32_t spilled = 0;  // stream bits already staged (multiple of 32); bits - spilled <= 128
+  bool staged = false;   // the whole stream is in the staging column (emit_block_wave)
   uint32_t *stage;
   // the staged word at stream bit `spilled`: window offset o = 128 - (bits - spilled) from the top
   __device__ __forceinline__ uint32_t window_word(uint32_t o, uint32_t a, uint32_t b) const {
@@ -315,6 +316,115 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
     if (two) emit_ac(k2, v2, prev, sink);
   }
   if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB
+}
+
+// Wave-parallel emission of one block h (wave-uniform): lane k codes zigzag coefficient k.
+// For blocks with many coefficients (noise, fine texture) the per-lane loop of emit_block
+// runs as long as the wave's longest block, with the other lanes idle; here the block's
+// symbols are formed side by side and placed by a prefix sum of their lengths.
+//   coefficients: exact_coef with the block's row-image words broadcast from lanes 0-31
+//                 (one ds_read of column h, then ds_bpermute per word)
+//   symbols:      lane k (nonzero) codes ZRL* + (run, size) + mantissa, run from the ballot
+//                 of nonzeros; lane 0 the DC; lane 63 the EOB when coefficient 63 is zero
+//   bits:         each lane's <= 59 bits ORed into the wave's LDS stream words (<= 3 per
+//                 lane), which then go to block h's staging column (pack_chunk reads it)
+// Returns the block's bit count.  Same bytes as emit_block (FFmpeg encode_block).
+__device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, int diff_h, int tab_h,
+                                                 const uint8_t *zz, const uint32_t *m2, const int *qc,
+                                                 const uint32_t *s_ac, const uint32_t *s_dc, uint32_t *s_hv,
+                                                 uint32_t *stage_w, int lane) {
+  const uint32_t wv = lane < 32 ? s_pk[lane * 64 + h] : 0u;
+  const int n = zz[lane], ro = n >> 3, c = n & 7;
+  const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
+  const uint4 mp = *(const uint4 *)(m2 + ro * 4);
+  const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
+  const bool dc_row = ro == 0 || ro == 4;
+  int acc = dc_row ? 8 : (1 << 16);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i) * 4 + (c >> 1)) << 2), (int)wv);
+    const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i + 1) * 4 + (c >> 1)) << 2), (int)wv);
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel) ^ 0x80008000u;
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc, false);
+  }
+  const int u = acc >> (dc_row ? 4 : 17);
+  int v = (__mul24(u, qc[c * 8 + ro]) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
+  if (lane == 0) v = 0;  // the DC is coded from diff_h
+  const uint64_t nz = __ballot(v != 0);
+  const uint32_t *act = s_ac + tab_h * 256;
+  uint64_t V = 0;
+  uint32_t L = 0;
+  if (v != 0) {
+    const uint64_t below = nz & ((1ull << lane) - 1ull);
+    int run = lane - (below ? 63 - (int)__builtin_clzll(below) : 0) - 1;
+    if (run >= 16) {
+      const uint32_t ez = act[0xf0];  // ZRL
+      const uint32_t zc = ez & 0xffffu, zl = ez >> 16;
+      while (run >= 16) {
+        V = (V << zl) | zc;
+        L += zl;
+        run -= 16;
+      }
+    }
+    const int a = v < 0 ? -v : v;
+    const int cat = 32 - __clz(a);
+    const uint32_t e = act[((run & 15) << 4) | cat];
+    const uint32_t cl = (e >> 16) + (uint32_t)cat;
+    V = (V << cl) | (((e & 0xffffu) << cat) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u)));
+    L += cl;
+  } else if (lane == 63) {  // EOB: coefficient 63 is zero
+    const uint32_t e = act[0x00];
+    V = e & 0xffffu;
+    L = e >> 16;
+  } else if (lane == 0) {
+    const int cat = dc_cat(diff_h);
+    const uint32_t e = s_dc[tab_h * 16 + cat];
+    V = ((e & 0xffffu) << cat) | ((uint32_t)(diff_h < 0 ? diff_h - 1 : diff_h) & ((1u << cat) - 1u));
+    L = (e >> 16) + (uint32_t)cat;
+  }
+  const uint32_t incl = wave_incl_scan(L, lane), off = incl - L, total = lane63(incl);
+  if (L) {  // bits [off, off + L): V's MSB at bit off & 31 of word off >> 5 (MSB first)
+    const uint32_t sh = 96u - (off & 31u) - L;  // 6..95: V << sh fits 96 bits
+    const uint64_t hi = sh >= 32u ? V << (sh - 32u) : V >> (32u - sh);
+    const uint32_t lo = sh >= 32u ? 0u : (uint32_t)(V << sh);
+    uint32_t *d = s_hv + (off >> 5);
+    atomicOr(d, (uint32_t)(hi >> 32));
+    if ((uint32_t)hi) atomicOr(d + 1, (uint32_t)hi);
+    if (lo) atomicOr(d + 2, lo);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint32_t nws = (total + 31u) >> 5;
+  if ((uint32_t)lane < nws) {
+    stage_w[lane * 64 + h] = s_hv[lane];
+    s_hv[lane] = 0u;
+  }
+  return total;
+}
+
+// Blocks of a chunk coded by emit_block_wave instead of per lane: the lanes whose candidate
+// count exceeds T, for the T in {4, 8, 16, 32} that minimises (wave-parallel blocks x 2 +
+// T, the per-lane loop's remaining length) -- a wave-parallel block costs about two
+// iterations of the per-lane loop -- if that beats the per-lane loop alone (its length
+// bounded by the smallest T no lane exceeds).  0: every block per lane.
+__device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
+  uint64_t hv[4];
+  int serial = 64;
+#pragma unroll
+  for (int k = 3; k >= 0; k--) {
+    hv[k] = __ballot(ncand > (4 << k));
+    if (!hv[k]) serial = 4 << k;
+  }
+  uint64_t best = 0ull;
+  int best_cost = serial;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int cost = 2 * __popcll(hv[k]) + (4 << k);
+    if (hv[k] && cost < best_cost) {
+      best_cost = cost;
+      best = hv[k];
+    }
+  }
+  return best;
 }
 
 // -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
@@ -488,7 +598,7 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
   const uint32_t lw = has ? (off + q.bits - 1) >> 5 : fw;
   uint32_t head = 0, tail = 0;
   if (has) {
-    if (q.bits <= 128) {
+    if (q.bits <= 128 && !q.staged) {
       // the block's words from its end: d[4] = word lw, d[4 - j] = word lw - j, i.e. the
       // right-aligned 128 bits shifted left by t, the free bits after the block in word lw
       const uint32_t t = (32u - ((off + q.bits) & 31u)) & 31u, sh = 32u - t;  // sh in 1..32
@@ -745,6 +855,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
   __shared__ uint32_t s_skip[12];                  // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
+  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
   // per wave: the current frame's histogram (kCount)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
 
@@ -767,6 +878,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
   uint32_t *s_pk = s_pk_all[wave];
+  uint32_t *s_hv = s_hv_all[MODE == kEmitDefault ? wave : 0];
+  if (MODE == kEmitDefault)
+    for (int i = lane; i < kStageWords; i += 64) s_hv[i] = 0u;
   uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
   if (MODE == kCount)
     for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
@@ -867,10 +981,25 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     ShiftSink q;
     q.act = s_ac + tab * 256;
     q.dct = s_dc + tab * 16;
-    q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
-    if (cur_active) {
+    uint32_t *stage_w = stage_all + (size_t)gw * 64 * kStageWords;
+    q.stage = stage_w + lane;
+    const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);
+    if (cur_active && !((wide >> lane) & 1ull)) {
       emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
       if (q.bits > 128) q.flush();
+    }
+    if (wide) {  // the heavy blocks, one wave-parallel block at a time
+      for (uint64_t hw = wide; hw; hw &= hw - 1) {
+        const int h = (int)__builtin_ctzll(hw);
+        const uint32_t nb = emit_block_wave(s_pk, h, __builtin_amdgcn_readlane(diff, h),
+                                            __builtin_amdgcn_readlane(tab, h), s_zz, s_m2, s_qc, s_ac, s_dc,
+                                            s_hv, stage_w, lane);
+        if (lane == h) {
+          q.bits = nb;
+          q.staged = true;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged words visible to pack_chunk's lanes
     }
     pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     if (tn < 0) break;

@@ -39,13 +39,14 @@ def main():
     import torch
     import bench
     from ffmpeg_distributed_amd import _lib
-    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    from ffmpeg_distributed_amd.testsrc import CONTENT
+    gen = CONTENT[os.environ.get("CONTENT", "testsrc")]
     W, H, DW, DH, Q, N, FULL, HUFF, _ = bench.WORKLOADS[os.environ.get("WL", "c2")]
     dev = torch.device("cuda", 0)
     pool = torch.empty((N, W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)), dtype=torch.uint8, device=dev)
     for i in range(0, N, 10):
         k = min(10, N - i)
-        pool[i:i + k] = testsrc2_i420_torch(W, H, i, k, dev, full_range=FULL)
+        pool[i:i + k] = gen(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
     encs = {}
     for name, _, _ in vs:
