@@ -402,10 +402,10 @@ __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, in
 }
 
 // Blocks of a chunk coded by emit_block_wave instead of per lane: the lanes whose candidate
-// count exceeds T, for the T in {4, 8, 16, 32} that minimises (wave-parallel blocks x 2 +
-// T, the per-lane loop's remaining length) -- a wave-parallel block costs about two
-// iterations of the per-lane loop -- if that beats the per-lane loop alone (its length
-// bounded by the smallest T no lane exceeds).  0: every block per lane.
+// count exceeds T, for the T in {4, 8, 16, 32} that minimises 4 x (wave-parallel blocks) + T
+// (T bounds the per-lane loop that remains; a wave-parallel block costs about four
+// candidates of it: factors 1, 2, 4, 6 and 8 were A/B'd on three contents), if that beats
+// the per-lane loop alone (bounded by the smallest T no lane exceeds).  0: all per lane.
 __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
   uint64_t hv[4];
   int serial = 64;
@@ -418,7 +418,7 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
   int best_cost = serial;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const int cost = 2 * __popcll(hv[k]) + (4 << k);
+    const int cost = 4 * __popcll(hv[k]) + (4 << k);
     if (hv[k] && cost < best_cost) {
       best_cost = cost;
       best = hv[k];

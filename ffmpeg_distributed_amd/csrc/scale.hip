@@ -72,8 +72,7 @@ __device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const in
   uint32_t lo = q[0];
   if (D4) {
     int ah = 0, al = 0;
-#pragma unroll
-    for (int k = 0; k < htaps; k += 4) {
+    for (int k = 0; k < htaps; k += 4) {  // (HT > 0: unrolled by the compiler)
       const uint32_t hi = q[(k >> 2) + 1];
       const int w = (int)__builtin_amdgcn_alignbit(hi, lo, sh);  // taps k..k+3, int8 p - 128
       lo = hi;
@@ -83,7 +82,6 @@ __device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const in
     return sws_range(min(ah + (al >> 7) + hs, 32767), range);
   }
   int acc = 0;
-#pragma unroll
   for (int k = 0; k < htaps; k += 4) {
     const uint32_t hi = q[(k >> 2) + 1];
     const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, sh);  // taps k..k+3 (bytes, LE)
