@@ -1036,9 +1036,25 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
   uint32_t *s_aux = s_aux_all[wave];
   const int nwaves = gridDim.x * kWavesPerWg, gw = blockIdx.x * kWavesPerWg + wave;
   int aux_frame = -1;
+  // the chunk's symbol count and first 4 records are loaded one chunk ahead (the records
+  // past a block's count are never used, and every one of them is inside the record array)
+  uint32_t n_nx = 0, e_nx[4] = {0u, 0u, 0u, 0u};
+  auto head = [&](int tt) {
+    int frame, chunk, bbase;
+    task_pos(g, tt, frame, chunk, bbase);
+    const int b = chunk * 64 + lane;
+    n_nx = b < g.seg_blocks ? symn[(size_t)tt * 64 + lane] : 0u;
+    const uint32_t *rec = syms + (size_t)tt * kSymCap * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < 4; i++) e_nx[i] = rec[i * 64];
+  };
+  if (gw < ntasks) head(gw);
   for (int t = gw; t < ntasks; t += nwaves) {
     int frame, chunk, bbase;
     task_pos(g, t, frame, chunk, bbase);
+    const uint32_t n = n_nx;
+    uint32_t e[4] = {e_nx[0], e_nx[1], e_nx[2], e_nx[3]};
+    if (t + nwaves < ntasks) head(t + nwaves);
     if (frame != aux_frame) {  // the frame's code tables into the wave's LDS
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = ftabs[(size_t)frame * kFrameTabWords + i];
@@ -1052,12 +1068,12 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
     q.act = s_aux + tab * 256;
     q.dct = s_aux + 512 + tab * 16;
     q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
-    const uint32_t n = active ? symn[(size_t)t * 64 + lane] : 0u;
     const uint32_t *rec = syms + (size_t)t * kSymCap * 64 + lane;
     for (uint32_t j0 = 0; j0 < n; j0 += 4) {
-      uint32_t e[4];
+      if (j0) {
 #pragma unroll
-      for (int i = 0; i < 4; i++) e[i] = j0 + i < n ? rec[(j0 + i) * 64] : 0u;
+        for (int i = 0; i < 4; i++) e[i] = j0 + i < n ? rec[(j0 + i) * 64] : 0u;
+      }
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         if (j0 + i >= n) break;

@@ -527,3 +527,42 @@ def _sweep(cases):
                             chroma=c["chroma"], rst=c["rst"])
         for i in range(c["n"]):
             assert got[i] == ref[i], (c, i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+@pytest.mark.parametrize("q,full", [(1, False), (3, True), (8, False), (20, True)])
+def test_wave_parallel_blocks_match_oracle(q, full):
+    """k_encode's wave-parallel emission (emit_block_wave, default tables): chunks with 1..14
+    heavy blocks among flat ones -- noise of amplitudes 2..128 (dense blocks with coefficient
+    63 set, and sparse ones with long zero runs, i.e. ZRLs), luma and chroma -- byte-equal to
+    the oracle."""
+    w, h, n = 512, 256, 2
+    rng = np.random.default_rng(1000 + q)
+    frames = []
+    for i in range(n):
+        y = np.full((h, w), 100, np.int32)
+        u = np.full((h // 2, w // 2), 120, np.int32)
+        v = np.full((h // 2, w // 2), 140, np.int32)
+        nmcu = (w // 16) * (h // 16)
+        for chunk0 in range(0, nmcu * 6, 64):  # per chunk of 64 blocks: 1..14 heavy blocks
+            for _ in range(int(rng.integers(1, 15))):
+                b = chunk0 + int(rng.integers(0, 64))
+                m, k = divmod(b, 6)
+                if m >= nmcu:
+                    continue
+                my, mx = divmod(m, w // 16)
+                amp = int(rng.choice([2, 4, 8, 32, 128]))
+                blk = rng.integers(-amp, amp + 1, (8, 8))
+                if k < 4:
+                    yy, xx = my * 16 + (k >> 1) * 8, mx * 16 + (k & 1) * 8
+                    y[yy:yy + 8, xx:xx + 8] += blk
+                else:
+                    c = u if k == 4 else v
+                    c[my * 8:my * 8 + 8, mx * 8:mx * 8 + 8] += blk
+        frames.append(pack_i420(y.clip(0, 255).astype(np.uint8), u.clip(0, 255).astype(np.uint8),
+                                v.clip(0, 255).astype(np.uint8)))
+    frames = np.stack(frames)
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=n) as enc:
+        got = enc.encode(frames)
+    ref = oracle_frames(frames, w, h, q, full)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
