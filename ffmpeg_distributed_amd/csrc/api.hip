@@ -452,6 +452,9 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   g.mbw = (w + g.lmw - 1) / g.lmw;
   const int mbh = (h + 15) / 16;
   g.nmcu = g.mbw * mbh;
+  g.mbw_magic = g.mbw > 1 ? (uint32_t)((((uint64_t)1 << 32) + (uint64_t)g.mbw - 1) / (uint64_t)g.mbw) : 0u;
+  if ((uint64_t)(g.nmcu + 64) * (uint64_t)g.mbw >= ((uint64_t)1 << 32))
+    return set_err(MJG_E_INVALID, "frame too large (%d MCUs)", g.nmcu);
   // RST: one segment per MCU row (mpegvideo clips the slice count to mb_height, so a
   // single-row picture has no restart markers)
   c->rst = (k.flags & MJG_F_RST) && mbh > 1;

@@ -74,6 +74,8 @@ struct EncGeom {
   int mbw, nmcu;       // MCUs per row, per frame
   int bpm;             // blocks per MCU (6 or 8)
   uint32_t bpm_magic;  // ceil(2^32 / bpm): b / bpm == umulhi(b, bpm_magic) for b < 2^29
+  uint32_t mbw_magic;  // ceil(2^32 / mbw) (0 when mbw == 1): m / mbw == umulhi(m, mbw_magic)
+                       // while m * mbw < 2^32 (the host checks (nmcu + 64) * mbw)
   int lmw, cmh;        // luma MCU width (16, 4:4:4: 8), chroma MCU height (8, 4:2:2/4:4:4: 16)
   int nseg, seg_blocks, nchunks;  // segments per frame, blocks / chunks per segment
   int y_stride, c_stride;
@@ -461,16 +463,20 @@ struct Src {
   int stride, pw, ph, x0, y0;
 };
 
-__device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s) {
+// The block's 8 rows when it is active, inside its plane and 8-byte aligned (returns true);
+// otherwise every row load reads `safe` (the frames' base, aligned and valid) and the caller
+// refetches with fetch_rows_edge.  Unconditional loads: no per-lane branch and no zeroing of
+// the row registers around them.
+__device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s, bool active, const uint8_t *safe) {
   const uint8_t *base = s.plane + (size_t)s.y0 * s.stride + s.x0;
-  const bool fast = (s.x0 + 8 <= s.pw) && (s.y0 + 8 <= s.ph) &&
+  const bool fast = active && (s.x0 + 8 <= s.pw) && (s.y0 + 8 <= s.ph) &&
                     ((((uintptr_t)base) | (uintptr_t)s.stride) & 7) == 0;
-  if (fast) {
-    // plain loads: a chunk's row segments straddle 64-B sectors shared with the
-    // neighbouring chunk, which L2 keeps for its wave (nontemporal loads read 1.64x)
+  const uint8_t *p = fast ? base : safe;
+  const size_t st = fast ? (size_t)s.stride : 0;
+  // plain loads: a chunk's row segments straddle 64-B sectors shared with the
+  // neighbouring chunk, which L2 keeps for its wave (nontemporal loads read 1.64x)
 #pragma unroll
-    for (int r = 0; r < 8; r++) raw[r] = *(const uint64_t *)(base + (size_t)r * s.stride);
-  }
+  for (int r = 0; r < 8; r++) raw[r] = *(const uint64_t *)(p + r * st);
   return fast;
 }
 
@@ -504,7 +510,7 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
   const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
   const int m = (int)__umulhi((uint32_t)b, g.bpm_magic);
   const uint32_t d = desc[b - m * g.bpm];
-  const int mx = m % g.mbw, my = m / g.mbw;
+  const int my = g.mbw == 1 ? m : (int)__umulhi((uint32_t)m, g.mbw_magic), mx = m - my * g.mbw;
   const int plane = (int)(d & 3u), dx = (int)((d >> 3) & 1u) * 8, dy = (int)((d >> 4) & 1u) * 8;
   Src s;
   if (plane == 0) {
@@ -905,7 +911,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   int b = chunk * 64 + lane;  // block in the segment
   bool active = b < nblk;
   uint64_t raw[8];
-  bool fast = active && fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc));
+  bool fast = fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc), active, frames);
   int carry = carry_finish(carry_row(frames, g, frame, bbase, chunk, lane, s_desc), chunk, lane, rc, g,
                            s_desc);
 
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       task_pos(g, tn, frame, chunk, bbase);
       b = chunk * 64 + lane;
       active = b < nblk;
-      fast = active && fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc));
+      fast = fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc), active, frames);
     }
     // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
     const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, bbase, chunk, lane, s_desc) : 0;
