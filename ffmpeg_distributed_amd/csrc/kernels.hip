@@ -89,7 +89,7 @@ struct EncGeom {
 __device__ __forceinline__ int desc_tab(uint32_t d) { return (int)((d >> 2) & 1u); }
 __device__ __forceinline__ int desc_delta(uint32_t d) { return (int)(d >> 8); }
 __device__ __forceinline__ int block_in_mcu(const EncGeom &g, int b) {
-  return b - g.bpm * (int)__umulhi((uint32_t)b, g.bpm_magic);
+  return b - __mul24(g.bpm, (int)__umulhi((uint32_t)b, g.bpm_magic));
 }
 
 
@@ -468,7 +468,8 @@ struct Src {
 // refetches with fetch_rows_edge.  Unconditional loads: no per-lane branch and no zeroing of
 // the row registers around them.
 __device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s, bool active, const uint8_t *safe) {
-  const uint8_t *base = s.plane + (size_t)s.y0 * s.stride + s.x0;
+  // row offset y0 * stride < the plane size < 2^32, operands < 2^24
+  const uint8_t *base = s.plane + ((uint32_t)__umul24((uint32_t)s.y0, (uint32_t)s.stride) + (uint32_t)s.x0);
   const bool fast = active && (s.x0 + 8 <= s.pw) && (s.y0 + 8 <= s.ph) &&
                     ((((uintptr_t)base) | (uintptr_t)s.stride) & 7) == 0;
   const uint8_t *p = fast ? base : safe;
@@ -509,8 +510,9 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
                                          const uint32_t *desc) {
   const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
   const int m = (int)__umulhi((uint32_t)b, g.bpm_magic);
-  const uint32_t d = desc[b - m * g.bpm];
-  const int my = g.mbw == 1 ? m : (int)__umulhi((uint32_t)m, g.mbw_magic), mx = m - my * g.mbw;
+  // (24-bit multiplies: every operand here is below 2^24)
+  const uint32_t d = desc[b - __mul24(m, g.bpm)];
+  const int my = g.mbw == 1 ? m : (int)__umulhi((uint32_t)m, g.mbw_magic), mx = m - __mul24(my, g.mbw);
   const int plane = (int)(d & 3u), dx = (int)((d >> 3) & 1u) * 8, dy = (int)((d >> 4) & 1u) * 8;
   Src s;
   if (plane == 0) {
@@ -518,7 +520,7 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
     s.stride = g.y_stride;
     s.pw = g.w;
     s.ph = g.h;
-    s.x0 = mx * g.lmw + dx;
+    s.x0 = __mul24(mx, g.lmw) + dx;
     s.y0 = my * 16 + dy;
   } else {
     s.plane = fr + (plane == 1 ? g.u_off : g.v_off);
@@ -526,7 +528,7 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
     s.pw = g.cw;
     s.ph = g.ch;
     s.x0 = mx * 8 + dx;
-    s.y0 = my * g.cmh + dy;
+    s.y0 = __mul24(my, g.cmh) + dy;
   }
   return s;
 }
@@ -865,7 +867,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   // per wave: the current frame's histogram (kCount)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
   if (tid < 32) s_dc[tid] = tabs[512 + tid];
   if (tid < 64) {
@@ -1036,7 +1038,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
     uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ stage_all, int ntasks) {
   __shared__ uint32_t s_aux_all[kWavesPerWg][kFrameTabWords];
   __shared__ uint32_t s_desc[8];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   if (tid < 8) s_desc[tid] = tabs[672 + tid];
   __syncthreads();
   uint32_t *s_aux = s_aux_all[wave];
