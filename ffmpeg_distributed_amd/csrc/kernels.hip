@@ -161,14 +161,14 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // Inclusive wave prefix sum on DPP lane moves (no LDS round trips): Hillis-Steele within
-// each 16-lane row (row_shr 1, 2, 4, 8; lanes whose source is outside the row add the
-// `old` 0), then row_bcast:15 carries row 0 / row 2 totals into rows 1 / 3 and
+// each 16-lane row (row_shr 1, 2, 4, 8; lanes whose source is outside the row read 0:
+// bound_ctrl, so each step is one v_add_u32_dpp), then row_bcast:15 carries row 0 / row 2 totals into rows 1 / 3 and
 // row_bcast:31 carries the rows 0-1 total into rows 2-3.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
