@@ -461,6 +461,11 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   g.nseg = c->rst ? mbh : 1;
   g.seg_blocks = (c->rst ? g.mbw : g.nmcu) * g.bpm;
   g.nchunks = (g.seg_blocks + 63) / 64;  // chunks of 64 blocks (one wave each) per segment
+  g.nchunks_magic = (((unsigned long long)1 << 40) + (unsigned long long)g.nchunks - 1) / (unsigned long long)g.nchunks;
+  g.nseg_magic = (((unsigned long long)1 << 40) + (unsigned long long)g.nseg - 1) / (unsigned long long)g.nseg;
+  // task t / nchunks by magic (exact while t * nchunks < 2^40, t < max_batch * nseg * nchunks)
+  if ((unsigned long long)k.max_batch * g.nseg * g.nchunks * g.nchunks >= ((unsigned long long)1 << 40))
+    return set_err(MJG_E_INVALID, "max_batch %d too large for this frame size", k.max_batch);
   g.y_stride = w;
   g.c_stride = cw;
   g.u_off = (long long)w * h;

@@ -78,6 +78,8 @@ struct EncGeom {
                        // while m * mbw < 2^32 (the host checks (nmcu + 64) * mbw)
   int lmw, cmh;        // luma MCU width (16, 4:4:4: 8), chroma MCU height (8, 4:2:2/4:4:4: 16)
   int nseg, seg_blocks, nchunks;  // segments per frame, blocks / chunks per segment
+  unsigned long long nchunks_magic, nseg_magic;  // ceil(2^40 / n): t / n == (t * magic) >> 40
+                                                 // for t * n < 2^40 (tasks per launch)
   int y_stride, c_stride;
   long long frame_stride, u_off, v_off;
   int range_convert;   // 1: yuv420p (tv) input without scale -> swscale tv->pc per pixel
@@ -535,14 +537,14 @@ __device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g
 
 // Task t (one chunk) -> frame, chunk index in its segment, first block of the segment.
 __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, int &chunk, int &bbase) {
-  const int seg = t / g.nchunks;
+  const int seg = (int)(((unsigned long long)(uint32_t)t * g.nchunks_magic) >> 40);
   chunk = t - seg * g.nchunks;
   if (g.nseg == 1) {  // one segment per frame (no RST): skip the second division
     frame = seg;
     bbase = 0;
     return;
   }
-  frame = seg / g.nseg;
+  frame = (int)(((unsigned long long)(uint32_t)seg * g.nseg_magic) >> 40);
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
