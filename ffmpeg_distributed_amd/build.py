@@ -65,15 +65,19 @@ def check() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and check():
         return LIB
-    cmd = _command(LIB + ".tmp")
+    # per-process temporaries and atomic renames: ranks of one node that find the library
+    # stale at the same time each build a complete copy, and none loads a partial file
+    tmp = f"{LIB}.tmp{os.getpid()}"
+    cmd = _command(tmp)
     if not shutil.which(cmd[0]) and not os.path.exists(cmd[0]):
         raise RuntimeError(f"{LIB} is missing or stale (sources changed) and {cmd[0]} is absent")
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    with open(STAMP, "w") as f:
+    os.replace(tmp, LIB)
+    with open(f"{STAMP}.tmp{os.getpid()}", "w") as f:
         f.write(source_digest() + "\n")
+    os.replace(f"{STAMP}.tmp{os.getpid()}", STAMP)
     return LIB
 
 
