@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +21,7 @@
 using namespace mjg;
 
 namespace {
+
 
 thread_local std::string g_err = "no error";
 
@@ -215,6 +217,7 @@ struct mjg_ctx {
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
   bool fused = false;   // -vf scale through k_scale_encode (no d_scaled)
+  bool dct_mfma = false;  // MJG_F_DCT_MFMA: k_encode<.., kEmitDefault, true>
   FusedGeom fgeom{};
   int fused_grid = 0;   // persistent k_scale_encode workgroups
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
@@ -408,6 +411,96 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   return MJG_OK;
 }
 
+// IEEE binary16 bits of x (normal range or 0), round to nearest even; `up`: the next value
+// away from zero when that rounding shrank |x|.
+uint16_t f16_bits(double x, bool up) {
+  if (x == 0.0) return 0;
+  const uint16_t sign = x < 0 ? 0x8000 : 0;
+  double a = std::fabs(x);
+  int e = (int)std::floor(std::log2(a));
+  if (std::ldexp(1.0, e) > a) e--;
+  if (std::ldexp(1.0, e + 1) <= a) e++;
+  double m = a / std::ldexp(1.0, e - 10);  // [1024, 2048)
+  double r = std::nearbyint(m);            // ties to even (default rounding mode)
+  if (up && r < m) r += 1.0;
+  if (r >= 2048.0) {
+    r /= 2.0;
+    e++;
+  }
+  return (uint16_t)(sign | (uint16_t)((e + 15) << 10) | (uint16_t)((int)r - 1024));
+}
+
+// MF k_encode's MFMA A fragments (kernels.hip dct_mfma), [frag][lane] x 4 words of f16 pairs.
+// A1 (pass 1, exact): the pass-1 matrix in two f16 digits; A2 (pass 2, screen): the pass-2
+// rows of zigzag coefficient z scaled by 2^10 / tau_z, where tau_z is the pass-2 sum below
+// which the coefficient quantises to zero minus a bound on the screen's error:
+//   * pass-1 outputs enter as f16(D), D = S/512 + 2^-10 unrounded: |f16(D) - y| <= 0.502 +
+//     2^-11 (|y| + 1), and 0 for outputs 0/4 (multiples of 16 below 2^15: exact);
+//   * the scaled coefficients are rounded (relative 2^-11); rows 0/4 (all +-1) round up
+//     in magnitude instead, a uniform scale that only widens the screen;
+//   * f32 accumulation (2^-18 of the worst-case sum, generous);
+// with |y| <= Ymax(c) = 16384 (outputs 0/4) or 128 * L1(pass-1 row c) / 512 + 1.
+int mf_fragments(const int32_t *qmat, uint32_t *out) {
+  static const int kDot[64] = MJG_PASS2_DOT;
+  auto c1 = [&](int i, int x) { return (i == 0 || i == 4) ? 16 * kDot[i * 8 + x] : kDot[i * 8 + x]; };
+  uint16_t f[12][64][8] = {};
+  for (int l = 0; l < 64; l++) {
+    const int m = l & 31, h = l >> 5;
+    // A1: fragment 2P + d, pattern P: output row r_loc = m >> 3 takes pixel row 2P + h
+    for (int P = 0; P < 2; P++)
+      for (int d = 0; d < 2; d++)
+        for (int j = 0; j < 8; j++) {
+          const int rl = m >> 3, i = m & 7;
+          if (rl != 2 * P + h) continue;
+          const int cv = c1(i, j);
+          double v;
+          if (i == 0 || i == 4) {
+            v = d == 0 ? cv : 0;
+          } else {
+            const int hi = (int)std::lround(cv / 64.0) * 64;
+            v = (d == 0 ? hi : cv - hi) / 512.0;
+          }
+          f[2 * P + d][l][j] = f16_bits(v, false);
+        }
+    // A2: fragment 4 + 4t + s
+    for (int t = 0; t < 2; t++) {
+      const int hz = (m >> 2) & 1, q = (m & 3) + 4 * (m >> 3);
+      const int z = 32 * hz + 31 - 16 * t - q;
+      const int nat = kZigzag[z], io = nat >> 3, col = nat & 7;
+      double scale = 1.0;
+      bool up = false;
+      if (z != 0) {
+        const long long qm = qmat[nat], T = ((5ll << 18) + qm - 1) / qm;
+        const bool dcrow = io == 0 || io == 4;
+        double l1 = 0, l1c = 0;
+        for (int r = 0; r < 8; r++) l1 += std::abs(kDot[io * 8 + r]);
+        for (int x = 0; x < 8; x++) l1c += std::abs(c1(col, x));
+        const bool exact_in = col == 0 || col == 4;
+        const double ymax = exact_in ? 16384.0 : 128.0 * l1c / 512.0 + 1.0;
+        const double eb = exact_in ? 0.0 : 0.502 + (ymax + 1.0) / 2048.0;
+        const double B = dcrow ? 16.0 * (double)T - 8.5 : (double)T * 131072.0 - 65536.0 - 0.5;
+        const double E = l1 * eb + (dcrow ? 0.0 : l1 * (ymax + eb) / 2048.0) + l1 * ymax / 262144.0;
+        const double tau = B - E;
+        if (tau < 1.0) return set_err(MJG_E_INVALID, "screen threshold %g for coefficient %d", tau, z);
+        scale = 1024.0 / tau;
+        up = dcrow;
+      }
+      for (int s = 0; s < 4; s++)
+        for (int j = 0; j < 8; j++) {
+          const int nd = 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+          const int r = 4 * (s >> 1) + (nd >> 3), i = nd & 7;
+          if (i != col) continue;
+          f[4 + 4 * t + s][l][j] = f16_bits(kDot[io * 8 + r] * scale, up);
+        }
+    }
+  }
+  for (int fr = 0; fr < 12; fr++)
+    for (int l = 0; l < 64; l++)
+      for (int e = 0; e < 4; e++)
+        out[(fr * 64 + l) * 4 + e] = (uint32_t)f[fr][l][2 * e] | ((uint32_t)f[fr][l][2 * e + 1] << 16);
+  return MJG_OK;
+}
+
 int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->device = device;
   c->cfg = *cfg;
@@ -484,6 +577,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
                         c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
+  c->dct_mfma = (k.flags & MJG_F_DCT_MFMA) && !c->optimal;
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
@@ -545,6 +639,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       for (int i = 0; i < 3; i++) tabs[680 + 3 * (jp - 1) + i] = lim[i];
     }
   }
+  if (int rc = mf_fragments(c->qmat, tabs + kMfTabOff)) return rc;
   // [672, 680): block-of-MCU descriptors in coding order (EncGeom): plane | chroma table << 2 |
   // dx8 << 3 | dy8 << 4 | DC predecessor distance << 8 (ff_mjpeg_encode_mb order; the
   // predecessor is the previous block of the same component)
@@ -639,7 +734,9 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // persistent k_encode / k_scale_encode grids: every CU filled with as many workgroups as fit
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, c->dct_mfma ? (const void *)k_encode<true, kEmitDefault, true> : (const void *)k_encode<true, kEmitDefault>,
+      64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
   size_t stage_cols = (size_t)c->enc_grid * kWavesPerWg;
   if (c->fused) {
@@ -710,17 +807,26 @@ void launch_fused(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
     range ? launch_fused3<4, 3, true, MODE>(c, S, src, n) : launch_fused3<4, 3, false, MODE>(c, S, src, n);
 }
 
-template <int MODE>
-void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+template <int MODE, bool MF>
+void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
   if (g.range_convert)
-    k_encode<true, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
+    k_encode<true, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         c->d_stage_bits, S.d_syms, S.d_symn);
   else
-    k_encode<false, MODE><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
+    k_encode<false, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         c->d_stage_bits, S.d_syms, S.d_symn);
+}
+
+// The DCT stage: the VALU passes, or (MJG_F_DCT_MFMA, -huffman default) dct_mfma.
+template <int MODE>
+void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+  if (MODE == kEmitDefault && c->dct_mfma)
+    launch_encode2<kEmitDefault, true>(c, S, enc_in, wgs, ntasks);
+  else
+    launch_encode2<MODE, false>(c, S, enc_in, wgs, ntasks);
 }
 
 }  // namespace

@@ -68,6 +68,12 @@ extern "C" {
                                   section 3b).  Ignored with MJG_F_DEBUG_COEFS, RST, non-4:2:0 or
                                   filters it does not handle */
 
+#define MJG_F_DCT_MFMA 256u    /* -huffman default: k_encode's two jfdctint passes on the matrix cores
+                                  (v_mfma_f32_32x32x16_f16: pass 1 exact in two f16 digits, pass 2
+                                  a quantiser screen), dct_mfma in kernels.hip.  Same bytes.
+                                  Opt-in: it ties the VALU passes on MI355X.
+                                  Ignored with MJG_F_HUFFMAN_OPTIMAL */
+
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */
 #define MJG_K_ENCODE 1         /* load [+ fused scale] + FDCT + quant + Huffman -> chunk bits */

@@ -515,13 +515,13 @@ def test_random_sweep_large_matches_oracle(part):
     _sweep(SWEEP_LARGE[part::4])
 
 
-def _sweep(cases):
+def _sweep(cases, **opts):
     for c in cases:
         w, h = c["w"], c["h"]
         dw, dh = c["scale"] or (None, None)
         frames = rand_frames(w, h, c["n"], seed=c["seed"], kind=c["kind"], chroma=c["chroma"])
         with MjpegEncoder(0, w, h, dw, dh, qscale=c["q"], full_range=c["full"], max_batch=c["batch"],
-                          huffman=c["huffman"], chroma=c["chroma"], rst=c["rst"]) as enc:
+                          huffman=c["huffman"], chroma=c["chroma"], rst=c["rst"], **opts) as enc:
             got = enc.encode(frames)
         ref = oracle_frames(frames, w, h, c["q"], c["full"], dw, dh, huffman=c["huffman"],
                             chroma=c["chroma"], rst=c["rst"])
@@ -566,3 +566,72 @@ def test_wave_parallel_blocks_match_oracle(q, full):
     ref = oracle_frames(frames, w, h, q, full)
     for i in range(n):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
+# ------------------------------------------- k_encode's DCT on the matrix cores (MJG_F_DCT_MFMA)
+# dct_mfma: pass 1 exact in two f16 digits, pass 2 a quantiser screen whose candidates are
+# quantised exactly (the same bytes), the permlane32 exchange and the zigzag mask.
+
+@pytest.mark.parametrize("part", range(4))
+def test_dct_mfma_random_sweep(part):
+    """Every -huffman default case of the 600-case random sweep (sizes, q 1..31, tv/pc,
+    six contents, 4:2:0/4:2:2/4:4:4, RST, scaling, ragged batches) through the MFMA DCT."""
+    _sweep([c for c in SWEEP if c["huffman"] == "default"][part::4], dct_mfma=True)
+
+
+def test_dct_mfma_large_sweep():
+    _sweep([c for c in SWEEP_LARGE if c["huffman"] == "default"], dct_mfma=True)
+
+
+@pytest.mark.parametrize("w,h,q", [(72, 40, 5), (1920, 1080, 3)])
+def test_dct_mfma_coefficients(w, h, q):
+    frames = rand_frames(w, h, 2, seed=1, kind="smooth" if w < 200 else "testsrc")
+    with MjpegEncoder(0, w, h, qscale=q, full_range=True, max_batch=2, debug_coefs=True,
+                      dct_mfma=True) as enc:
+        enc.submit(frames)
+        enc.sync()
+        for i in range(2):
+            y, u, v = split_i420(frames[i], w, h)
+            ref, _ = oracle.frame_coeffs(y, u, v, q)
+            bad = np.nonzero((enc.debug_coefs(i) != ref).any(1))[0]
+            assert bad.size == 0, (i, bad[:10])
+
+
+@pytest.mark.parametrize("q,full", [(1, False), (31, True)])
+def test_dct_mfma_extremes(q, full):
+    """Extreme blocks for the screen's error bound: full-swing checkers (pass-1 outputs
+    near 2^14), black/white blocks, noise, at the finest and coarsest quantiser."""
+    w, h = 256, 128
+    rng = np.random.default_rng(q)
+    y = np.where((np.arange(w)[None, :] // 1 + np.arange(h)[:, None]) % 2, 255, 0).astype(np.uint8)
+    y[:, 64:128] = rng.integers(0, 256, (h, 64))
+    y[:, 128:160] = 255
+    y[:, 160:192] = 0
+    y[:, 192:] = np.where((np.arange(64)[None, :] // 4) % 2, 255, 0)
+    u = rng.integers(0, 256, (h // 2, w // 2)).astype(np.uint8)
+    v = np.where(np.arange(w // 2)[None, :] % 2, 0, 255).repeat(h // 2, 0).astype(np.uint8)
+    frames = np.stack([pack_i420(y, u, v)])
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=1, dct_mfma=True) as enc:
+        got = enc.encode(frames)
+    assert got[0] == oracle_frames(frames, w, h, q, full)[0]
+
+
+def test_dct_mfma_4k_segment_from_device_memory():
+    """BASELINE configs[1] as the bench submits it, through the MFMA DCT: a 120-frame 4K
+    segment by device pointer, every frame byte-equal to the oracle."""
+    import torch
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    w, h, n = 3840, 2160, 120
+    dev = torch.device("cuda", 0)
+    pool = torch.empty((n, i420_frame_bytes(w, h)), dtype=torch.uint8, device=dev)
+    for i in range(0, n, 20):
+        pool[i:i + 20] = testsrc2_i420_torch(w, h, 2000 + i, 20, dev)
+    torch.cuda.synchronize()
+    host = pool.cpu().numpy()
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=n, dct_mfma=True) as enc:
+        enc.submit(device_ptr=pool.data_ptr(), nframes=n)
+        enc.sync()
+        a = enc.fetch()
+    ref = _oracle_many(host, w, h, qscale=5)
+    for i in range(n):
+        assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))

@@ -53,9 +53,11 @@ def main():
         _lib._lib = None
         _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
         from ffmpeg_distributed_amd.encoder import MjpegEncoder
-        # a name ending in "_f" runs the -vf scale leg as the fused k_scale_encode (MJG_F_FUSED)
+        # a name ending in "_f" runs the -vf scale leg as the fused k_scale_encode (MJG_F_FUSED),
+        # one ending in "_m" k_encode's MFMA DCT stage (MJG_F_DCT_MFMA)
         encs[name] = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, timing=True,
-                                  huffman=HUFF, fused=name.endswith("_f"))
+                                  huffman=HUFF, fused=name.endswith("_f"),
+                                  dct_mfma=name.endswith("_m"))
     res = {n: [] for n in encs}
     ref = None
     for rnd in range(6):
