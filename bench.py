@@ -67,8 +67,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--fused", action="store_true",
                    help="-vf scale configs: the opt-in fused k_scale_encode instead of k_scale + k_encode")
-    p.add_argument("--dct-mfma", action="store_true",
-                   help="-huffman default: the opt-in MFMA DCT stage of k_encode (MJG_F_DCT_MFMA)")
+    p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
+                   help="-huffman default: k_encode's DCT stage (auto: the matrix cores with -vf scale)")
     p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
     p.add_argument("--kernel-timing-detail", action="store_true",
                    help="events around every tail kernel too (adds ~10 us idle per event)")
@@ -269,7 +269,8 @@ def main():
 
     enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg,
                        timing=False if a.no_kernel_timing else ("detail" if a.kernel_timing_detail else True),
-                       huffman=HUFF, rst=a.rst, fused=a.fused, dct_mfma=a.dct_mfma)
+                       huffman=HUFF, rst=a.rst, fused=a.fused,
+                       dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
     bytes_out = []
 
     # Segments are pipelined two deep (mjg_submit queues up to two): segment s+1's kernels
@@ -302,7 +303,7 @@ def main():
     frames_total = a.steps * seg * world
     value = frames_total / dt
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
-    pmc = load_pmc(a.workload, a.content) if (seg == SEG and not a.rst and not a.fused and not a.dct_mfma
+    pmc = load_pmc(a.workload, a.content) if (seg == SEG and not a.rst and not a.fused and a.dct == "auto"
                                               and HUFF == WORKLOADS[a.workload][7]) else {}
     primary, per_kernel = rooflines(kt, seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H))
     primary = dict(primary, launches=nl)
@@ -339,7 +340,9 @@ def main():
                        + (" -slices 8" if a.rst else ""),
                        **({"scale_kernels": "k_scale_encode (fused)" if a.fused else "k_scale + k_encode"}
                           if (DW, DH) != (W, H) else {}),
-                       **({"dct": "MFMA (MJG_F_DCT_MFMA)"} if a.dct_mfma and HUFF == "default" else {})},
+                       "dct": "VALU (k_encode<.., optimal counting pass>)" if HUFF == "optimal" else
+                              ("matrix cores (dct_mfma)" if a.dct == "mfma" or (a.dct == "auto" and (DW, DH) != (W, H))
+                               else "VALU (row_pass + column_screen)")},
             "roofline": primary,
             "roofline_kernels": per_kernel,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},

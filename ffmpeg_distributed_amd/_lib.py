@@ -29,6 +29,7 @@ MJG_F_RST = 32
 MJG_F_TIMING_DETAIL = 64
 MJG_F_FUSED = 128
 MJG_F_DCT_MFMA = 256
+MJG_F_DCT_VALU = 512
 
 # mjg_config.chroma_format
 CHROMA_FORMATS = {"420": 0, "422": 1, "444": 2}

@@ -217,7 +217,7 @@ struct mjg_ctx {
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
   bool fused = false;   // -vf scale through k_scale_encode (no d_scaled)
-  bool dct_mfma = false;  // MJG_F_DCT_MFMA: k_encode<.., kEmitDefault, true>
+  bool dct_mfma = false;  // k_encode's DCT stage on the matrix cores (dct_mfma)
   FusedGeom fgeom{};
   int fused_grid = 0;   // persistent k_scale_encode workgroups
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
@@ -577,7 +577,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
                         c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
-  c->dct_mfma = (k.flags & MJG_F_DCT_MFMA) && !c->optimal;
+  // -huffman default: MFMA when the encode input is k_scale's output (measured faster there,
+  // DESIGN.md section 4c), or forced either way by the flags
+  c->dct_mfma = !c->optimal && !(k.flags & MJG_F_DCT_VALU) &&
+                ((k.flags & MJG_F_DCT_MFMA) || c->scale);
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
@@ -820,7 +823,7 @@ void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int nta
         c->d_stage_bits, S.d_syms, S.d_symn);
 }
 
-// The DCT stage: the VALU passes, or (MJG_F_DCT_MFMA, -huffman default) dct_mfma.
+// The DCT stage: the VALU passes, or (-huffman default) dct_mfma.
 template <int MODE>
 void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
   if (MODE == kEmitDefault && c->dct_mfma)

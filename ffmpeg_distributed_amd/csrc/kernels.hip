@@ -927,8 +927,9 @@ __device__ __forceinline__ uint32_t dct_group(const uint32_t (&rows)[4][2], int 
   uint4 bp[4];
 #pragma unroll
   for (int s = 0; s < 4; s++) bp[s] = pix_frag<RC>(rows[s][0], rows[s][1], tab, s_rc);
-  const uint4 p0h = s_f[0 * 64 + lane], p0l = s_f[1 * 64 + lane], p1h = s_f[2 * 64 + lane],
-              p1l = s_f[3 * 64 + lane];
+  // pattern P1 (output row r_loc = 2 + h) is P0 (r_loc = h) moved by 16 lanes: lane l ^ 16
+  const uint4 p0h = s_f[0 * 64 + lane], p0l = s_f[1 * 64 + lane], p1h = s_f[0 * 64 + (lane ^ 16)],
+              p1l = s_f[1 * 64 + (lane ^ 16)];
   f32x16 d[2];
 #pragma unroll
   for (int t = 0; t < 2; t++) {
@@ -1012,6 +1013,7 @@ __device__ __forceinline__ uint64_t dct_mfma(const uint64_t (&raw)[8], int tab, 
   return (((uint64_t)w1 << 32) | w0) & ~1ull;
 }
 
+// MF: the DCT stage on the matrix cores (dct_mfma) instead of row_pass + column_screen.
 template <bool RC, int MODE, bool MF = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
@@ -1023,17 +1025,18 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
-  __shared__ __attribute__((aligned(16))) float s_thr[64];    // screening thresholds^2 [col][row]
+  constexpr bool SCR = !MF;  // the VALU column screen
+  __shared__ __attribute__((aligned(16))) float s_thr[SCR ? 64 : 4];  // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
-  __shared__ uint8_t s_scat[64];  // candidate bit -> zigzag index (kScreenScatter)
+  __shared__ uint8_t s_scat[SCR ? 64 : 4];  // candidate bit -> zigzag index (kScreenScatter)
   __shared__ uint8_t s_rc[RC ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
-  __shared__ uint4 s_f[MF ? 12 * 64 : 1];          // MF: MFMA A fragments (dct_mfma)
+  __shared__ uint4 s_f[MF ? 12 * 64 : 1];  // MFMA A fragments (dct_mfma): [0, 2) pass 1, [4, 12) pass 2
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
-  __shared__ uint32_t s_skip[12];                  // column-skip limits, 3 u16x2 words per pair
+  __shared__ uint32_t s_skip[SCR ? 12 : 1];        // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
   // per wave: the current frame's histogram (kCount)
-  __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][kFrameTabWords];
+  __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][MODE == kEmitDefault ? 1 : kFrameTabWords];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
@@ -1041,15 +1044,15 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
-    s_thr[tid] = __uint_as_float(tabs[608 + tid]);
+    if (SCR) s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
       s_m2[tid] = (uint32_t)(uint16_t)kPass2Dot[2 * tid] | ((uint32_t)(uint16_t)kPass2Dot[2 * tid + 1] << 16);
-    s_scat[tid] = kScreenScatter[tid];
+    if (SCR) s_scat[tid] = kScreenScatter[tid];
   }
   if (tid < 8) {
     s_desc[tid] = tabs[672 + tid];
   }
-  if (tid < 12) s_skip[tid] = tabs[680 + tid];
+  if (SCR && tid < 12) s_skip[tid] = tabs[680 + tid];
   if (MF)
     for (int i = tid; i < 12 * 64; i += 64 * kWavesPerWg) s_f[i] = ((const uint4 *)(tabs + kMfTabOff))[i];
   if (RC)
@@ -1117,7 +1120,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
 
     uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
     if (cur_active) {
-      if (!MF) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
+      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
       if (g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
@@ -1129,7 +1132,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
         }
       }
     }
-    if (!MF) mask = screen_mask(ca, cb, s_scat);
+    if (SCR) mask = screen_mask(ca, cb, s_scat);
 
     // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.

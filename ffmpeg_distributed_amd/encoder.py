@@ -56,7 +56,7 @@ class MjpegEncoder:
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
                  debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
                  huffman: str = "default", chroma: str = "420", rst: bool = False,
-                 fused: bool = False, dct_mfma: bool = False):
+                 fused: bool = False, dct_mfma: Optional[bool] = None):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -82,8 +82,12 @@ class MjpegEncoder:
             flags |= _lib.MJG_F_RST
         if fused:  # -vf scale as one kernel, k_scale_encode (opt-in: slower on MI355X)
             flags |= _lib.MJG_F_FUSED
-        if dct_mfma:  # k_encode's DCT on the matrix cores (opt-in: ties the VALU passes on MI355X)
+        # k_encode's DCT stage: None = the library's choice (matrix cores with -vf scale),
+        # True = the matrix cores, False = the VALU passes
+        if dct_mfma is True:
             flags |= _lib.MJG_F_DCT_MFMA
+        elif dct_mfma is False:
+            flags |= _lib.MJG_F_DCT_VALU
         self.huffman = huffman
         self.chroma = str(chroma)
         if self.chroma not in _lib.CHROMA_FORMATS:

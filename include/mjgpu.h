@@ -70,9 +70,10 @@ extern "C" {
 
 #define MJG_F_DCT_MFMA 256u    /* -huffman default: k_encode's two jfdctint passes on the matrix cores
                                   (v_mfma_f32_32x32x16_f16: pass 1 exact in two f16 digits, pass 2
-                                  a quantiser screen), dct_mfma in kernels.hip.  Same bytes.
-                                  Opt-in: it ties the VALU passes on MI355X.
-                                  Ignored with MJG_F_HUFFMAN_OPTIMAL */
+                                  a quantiser screen), dct_mfma in kernels.hip.  Same bytes.  The
+                                  default with -vf scale (measured faster there); this flag forces
+                                  it for unscaled input */
+#define MJG_F_DCT_VALU 512u    /* -huffman default: the VALU passes even with -vf scale (A/B) */
 
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */

@@ -572,22 +572,27 @@ def test_wave_parallel_blocks_match_oracle(q, full):
 # dct_mfma: pass 1 exact in two f16 digits, pass 2 a quantiser screen whose candidates are
 # quantised exactly (the same bytes), the permlane32 exchange and the zigzag mask.
 
+@pytest.mark.parametrize("mode", [True, False])
 @pytest.mark.parametrize("part", range(4))
-def test_dct_mfma_random_sweep(part):
+def test_dct_mfma_random_sweep(part, mode):
     """Every -huffman default case of the 600-case random sweep (sizes, q 1..31, tv/pc,
-    six contents, 4:2:0/4:2:2/4:4:4, RST, scaling, ragged batches) through the MFMA DCT."""
-    _sweep([c for c in SWEEP if c["huffman"] == "default"][part::4], dct_mfma=True)
+    six contents, 4:2:0/4:2:2/4:4:4, RST, scaling, ragged batches) with k_encode's DCT stage
+    forced onto the matrix cores (True) or the VALU (False; the library's default picks
+    the matrix cores for scaled input and the VALU otherwise, which the plain sweep covers)."""
+    _sweep([c for c in SWEEP if c["huffman"] == "default"][part::4], dct_mfma=mode)
 
 
-def test_dct_mfma_large_sweep():
-    _sweep([c for c in SWEEP_LARGE if c["huffman"] == "default"], dct_mfma=True)
+@pytest.mark.parametrize("mode", [True, False])
+def test_dct_mfma_large_sweep(mode):
+    _sweep([c for c in SWEEP_LARGE if c["huffman"] == "default"], dct_mfma=mode)
 
 
+@pytest.mark.parametrize("mode", [True, False])
 @pytest.mark.parametrize("w,h,q", [(72, 40, 5), (1920, 1080, 3)])
-def test_dct_mfma_coefficients(w, h, q):
+def test_dct_mfma_coefficients(w, h, q, mode):
     frames = rand_frames(w, h, 2, seed=1, kind="smooth" if w < 200 else "testsrc")
     with MjpegEncoder(0, w, h, qscale=q, full_range=True, max_batch=2, debug_coefs=True,
-                      dct_mfma=True) as enc:
+                      dct_mfma=mode) as enc:
         enc.submit(frames)
         enc.sync()
         for i in range(2):
@@ -597,8 +602,9 @@ def test_dct_mfma_coefficients(w, h, q):
             assert bad.size == 0, (i, bad[:10])
 
 
+@pytest.mark.parametrize("mode", [True, False])
 @pytest.mark.parametrize("q,full", [(1, False), (31, True)])
-def test_dct_mfma_extremes(q, full):
+def test_dct_mfma_extremes(q, full, mode):
     """Extreme blocks for the screen's error bound: full-swing checkers (pass-1 outputs
     near 2^14), black/white blocks, noise, at the finest and coarsest quantiser."""
     w, h = 256, 128
@@ -611,7 +617,7 @@ def test_dct_mfma_extremes(q, full):
     u = rng.integers(0, 256, (h // 2, w // 2)).astype(np.uint8)
     v = np.where(np.arange(w // 2)[None, :] % 2, 0, 255).repeat(h // 2, 0).astype(np.uint8)
     frames = np.stack([pack_i420(y, u, v)])
-    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=1, dct_mfma=True) as enc:
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=1, dct_mfma=mode) as enc:
         got = enc.encode(frames)
     assert got[0] == oracle_frames(frames, w, h, q, full)[0]
 

@@ -8,12 +8,12 @@ TAG=$1; CASES=${2:-"c2:testsrc c5:testsrc c4:testsrc c2:natural c2:noise-patches
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -40 $O/gpu_tests.txt; exit 1; }
-tail -2 $O/gpu_tests.txt
+[ -n "$NOTEST" ] || timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -40 $O/gpu_tests.txt; exit 1; }
+[ -n "$NOTEST" ] || tail -2 $O/gpu_tests.txt
 for c in $CASES; do
-  wl=${c%%:*}; ct=${c##*:}
-  echo "== $wl $ct"
-  WL=$wl CONTENT=$ct VARIANTS="${AB:-valu=:;mf_m=:}" timeout -k 10 200 python tools/variants.py > $O/ab_${wl}_${ct}.txt 2>&1 || { tail -20 $O/ab_${wl}_${ct}.txt; exit 1; }
-  cat $O/ab_${wl}_${ct}.txt
+  IFS=: read wl ct qq <<< "$c"
+  echo "== $wl $ct q${qq:-default}"
+  Q=${qq:-} WL=$wl CONTENT=$ct VARIANTS="${AB:-valu_v=:;mf_m=:}" timeout -k 10 200 python tools/variants.py > $O/ab_${wl}_${ct}${qq}.txt 2>&1 || { tail -20 $O/ab_${wl}_${ct}${qq}.txt; exit 1; }
+  grep median $O/ab_${wl}_${ct}${qq}.txt
 done
 echo done

@@ -42,6 +42,7 @@ def main():
     from ffmpeg_distributed_amd.testsrc import CONTENT
     gen = CONTENT[os.environ.get("CONTENT", "testsrc")]
     W, H, DW, DH, Q, N, FULL, HUFF, _ = bench.WORKLOADS[os.environ.get("WL", "c2")]
+    Q = int(os.environ.get("Q") or Q)  # quantiser override (A/B at other q)
     dev = torch.device("cuda", 0)
     pool = torch.empty((N, W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)), dtype=torch.uint8, device=dev)
     for i in range(0, N, 10):
@@ -54,10 +55,10 @@ def main():
         _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
         from ffmpeg_distributed_amd.encoder import MjpegEncoder
         # a name ending in "_f" runs the -vf scale leg as the fused k_scale_encode (MJG_F_FUSED),
-        # one ending in "_m" k_encode's MFMA DCT stage (MJG_F_DCT_MFMA)
+        # "_m" / "_v" force k_encode's DCT stage onto the matrix cores / the VALU
         encs[name] = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, timing=True,
                                   huffman=HUFF, fused=name.endswith("_f"),
-                                  dct_mfma=name.endswith("_m"))
+                                  dct_mfma=True if name.endswith("_m") else False if name.endswith("_v") else None)
     res = {n: [] for n in encs}
     ref = None
     for rnd in range(6):
