@@ -549,7 +549,10 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
-constexpr int kBatch = 16;  // chunks per work unit pulled from the counter (8 ties, 32 is 5% slower)
+// chunks per work unit pulled from the counter: 16 for the VALU DCT stage, 8 for the MFMA stage
+// (3 waves per SIMD, fewer chunks per wave), each the faster on its BASELINE configs
+template <bool MF>
+constexpr int kBatchOf = MF ? 8 : 16;
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
 // quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
@@ -1070,17 +1073,17 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
 
   const int nwaves = gridDim.x * kWavesPerWg;
   const int gw = blockIdx.x * kWavesPerWg + wave;
+  constexpr int kBatch = kBatchOf<MF>;
   const int nbatch = (ntasks + kBatch - 1) / kBatch;
   if (gw >= nbatch) return;
   const int nblk = g.seg_blocks;  // blocks of one entropy-coded segment
   constexpr bool rc = RC;
 
-  // Batches of kBatch consecutive chunks: the first one static (batch gw), the rest
+  // Units of kBatch consecutive chunks: the first one static (unit gw), the rest
   // pulled from work_ctr (zeroed by k_scan_bits after every launch), so waves whose
   // picture content is cheap take more batches and all waves finish together.
   int t = gw * kBatch, tend = min(t + kBatch, ntasks);
-  uint32_t nb = 0;  // lane 0: the batch after this one
-  if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
+  uint32_t nb = 0;  // lane 0: the unit after this one
   int frame, chunk, bbase;
   task_pos(g, t, frame, chunk, bbase);
   int b = chunk * 64 + lane;  // block in the segment
@@ -1091,6 +1094,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
                            s_desc);
 
   while (true) {
+    // the next unit is reserved at the top of this unit's last chunk (its rows are prefetched
+    // midway through it), not when this unit starts: a wave holding a reserved unit while the
+    // counter runs dry left the others idle for up to a whole unit at the end of every launch
+    if (t + 1 == tend && lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
     const uint32_t dsc = s_desc[block_in_mcu(g, b)];
     const int tab = desc_tab(dsc);
     if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, bbase + b, s_desc));
@@ -1158,7 +1165,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       if (new_batch) {
         carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
         tend = min(tn + kBatch, ntasks);
-        if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
       }
       t = tn;
       continue;
@@ -1191,7 +1197,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     if (new_batch) {
       carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
       tend = min(tn + kBatch, ntasks);
-      if (lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
     }
     t = tn;
   }
