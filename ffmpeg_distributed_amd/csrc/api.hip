@@ -156,6 +156,7 @@ struct PlaneScale {
   ScaleGeom g{};
   size_t lds = 0;
   dim3 grid;
+  int th = 32;  // k_scale tile height (64: the 2:1 filters, scale.hip)
   // k_scale_encode tables (kFusedTabWords per entry): h per scaled column: D4 words, [6] tap
   // position, [7] tap sum; v per scaled row: [0] first row pair, [1..npv] coefficient pairs
   uint32_t *d_fh = nullptr, *d_fv = nullptr;
@@ -343,25 +344,37 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
     p.fv[(size_t)y * kFusedTabWords] = (uint32_t)vps[y];
     for (int k = 0; k < npv && k < 7; k++) p.fv[(size_t)y * kFusedTabWords + 1 + k] = (uint32_t)vcp[(size_t)y * npv + k];
   }
-  int max_pairs = 0, max_nw = 0;
-  for (int y0 = 0; y0 < dh; y0 += kScaleTileH) {
-    const int ye = std::min(y0 + kScaleTileH, dh);
-    max_pairs = std::max(max_pairs, vps[ye - 1] + npv - vps[y0]);
-  }
+  // k_scale's tile height: 64 rows for the 2:1 filters when every window fits the fast path
+  // at a 36-dword row stride (scale.hip), else 32
+  auto tile_pairs = [&](int th) {
+    int m = 0;
+    for (int y0 = 0; y0 < dh; y0 += th) m = std::max(m, vps[std::min(y0 + th, dh) - 1] + npv - vps[y0]);
+    return m;
+  };
+  int max_nw = 0;
   for (int x0 = 0; x0 < dw; x0 += kScaleTileW) {  // same formula as k_scale's window
     const int xe = std::min(x0 + kScaleTileW, dw), cb = p.hf.pos[x0] & ~3;
     max_nw = std::max(max_nw, ((((p.hf.pos[xe - 1] + ht - cb + 3) >> 2) + 1) + 3) & ~3);
   }
+  const int th = (ht == 8 && npv == 5 && max_nw <= kScaleAliasWords && sw >= 16 &&
+                  2 * tile_pairs(64) <= 4 * scale_loads_per_wave(64) * kScaleLoadRows) ? 64 : 32;
+  const int max_pairs = tile_pairs(th);
+  p.th = th;
   ScaleGeom &g = p.g;
   g.htaps = ht;
   g.vtaps = vt;
   g.npv = npv;
   g.lds_pairs = max_pairs;
-  g.lds_win_words = 2 * max_pairs * max_nw;
-  p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW + (size_t)kScaleTileH * (npv + 1)) * 4;
+  if (th == 64) {  // pair image over the window rows (scale.hip: ALIAS)
+    g.lds_win_words = 2 * max_pairs * kScaleAliasWords;
+    p.lds = ((size_t)g.lds_win_words + (size_t)th * (npv + 1)) * 4;
+  } else {
+    g.lds_win_words = 2 * max_pairs * max_nw;
+    p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW + (size_t)th * (npv + 1)) * 4;
+  }
   if (p.lds > 64 * 1024)
     return set_err(MJG_E_INVALID, "scale ratio too large for one LDS tile (%zu B)", p.lds);
-  p.grid = dim3((dw + kScaleTileW - 1) / kScaleTileW, (dh + kScaleTileH - 1) / kScaleTileH, 1);
+  p.grid = dim3((dw + kScaleTileW - 1) / kScaleTileW, (dh + th - 1) / th, 1);
   int rc;
   if ((rc = dmalloc(&p.hcp, hcp.size())) || (rc = dmalloc(&p.hp, (size_t)dw)) ||
       (rc = dmalloc(&p.vcp, vcp.size())) || (rc = dmalloc(&p.vps, (size_t)dh)) ||
@@ -926,31 +939,33 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       }
       dim3 grid = ps.grid;
       grid.z = n;
-#define MJG_SCALE_LAUNCH3(HT, NPV, D4)                                                            \
-  do {                                                                                            \
-    if (sg.range == 1)                                                                            \
-      k_scale<HT, NPV, D4, 1><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
-                                                                ps.vcp, ps.vps, ps.hsum);         \
-    else if (sg.range == 2)                                                                       \
-      k_scale<HT, NPV, D4, 2><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
-                                                                ps.vcp, ps.vps, ps.hsum);         \
-    else                                                                                          \
-      k_scale<HT, NPV, D4, 0><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp, ps.hp, \
-                                                                ps.vcp, ps.vps, ps.hsum);         \
+#define MJG_SCALE_LAUNCH3(HT, NPV, D4, TH)                                                          \
+  do {                                                                                              \
+    if (sg.range == 1)                                                                              \
+      k_scale<HT, NPV, D4, 1, TH><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum); \
+    else if (sg.range == 2)                                                                         \
+      k_scale<HT, NPV, D4, 2, TH><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum); \
+    else                                                                                            \
+      k_scale<HT, NPV, D4, 0, TH><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum); \
   } while (0)
-#define MJG_SCALE_LAUNCH(HT, NPV)      \
-  do {                                 \
-    if (ps.d4)                         \
-      MJG_SCALE_LAUNCH3(HT, NPV, true);  \
-    else                               \
-      MJG_SCALE_LAUNCH3(HT, NPV, false); \
+#define MJG_SCALE_LAUNCH(HT, NPV, TH)      \
+  do {                                     \
+    if (ps.d4)                             \
+      MJG_SCALE_LAUNCH3(HT, NPV, true, TH);  \
+    else                                   \
+      MJG_SCALE_LAUNCH3(HT, NPV, false, TH); \
   } while (0)
-      if (sg.htaps == 8 && sg.npv == 5)  // 2:1 downscale (4K -> 1080p)
-        MJG_SCALE_LAUNCH(8, 5);
+      if (sg.htaps == 8 && sg.npv == 5 && ps.th == 64)  // 2:1 downscale (4K -> 1080p), 64-row tiles
+        MJG_SCALE_LAUNCH(8, 5, 64);
+      else if (sg.htaps == 8 && sg.npv == 5)
+        MJG_SCALE_LAUNCH(8, 5, 32);
       else if (sg.htaps == 4 && sg.npv == 3)  // upscale / mild downscale
-        MJG_SCALE_LAUNCH(4, 3);
+        MJG_SCALE_LAUNCH(4, 3, 32);
       else
-        MJG_SCALE_LAUNCH(0, 0);
+        MJG_SCALE_LAUNCH(0, 0, 32);
 #undef MJG_SCALE_LAUNCH
 #undef MJG_SCALE_LAUNCH3
     }

@@ -5,7 +5,12 @@
 //   lumRangeToJpeg_c / chrRangeToJpeg_c on that int16       (tv -> pc, if requested)
 //   yuv2planeX_8_c: clip_u8(((64 << 12) + sum h*f) >> 19)  (12-bit coeffs, flat dither)
 //
-// One workgroup = a 64 x 32 output tile (4 waves, lane = output column).
+// One workgroup = a 64 x TH output tile (4 waves, lane = output column).  TH = 64 for the 2:1
+// filters (8 h taps, 5 v pairs: 4K -> 1080p, windows of <= 36 dwords x 140 rows; the host
+// checks) with the row-pair image written over the window rows it was computed from (a
+// pair's two rows are read only by the wave that writes it, in program order), so the LDS of
+// a 64-row tile is that of the 32-row one, and rows at a fixed 36-dword stride (pair stride
+// 72: constant LDS offsets in the v-pass); TH = 32 otherwise.
 //   load:   the tile's source window (rows x dword-aligned columns, rows padded to 16-byte
 //           pieces) is staged in LDS from 16-byte loads, 7 rows x 9 pieces per wave-instruction,
 //           all issued before any is waited on.  (Measured on MI355X, c4: a persistent
@@ -32,8 +37,9 @@ namespace mjg {
 typedef short short2_t __attribute__((ext_vector_type(2)));
 
 constexpr int kScaleTileW = 64;
-constexpr int kScaleTileH = 32;
-constexpr int kScaleLoadRows = 7, kScaleLoadsPerWave = 3;  // fast window path: 84 rows x 9 pieces
+constexpr int kScaleLoadRows = 7;  // fast window path: rows x 9 pieces per wave-instruction
+__host__ __device__ constexpr int scale_loads_per_wave(int th) { return th == 64 ? 5 : 3; }
+constexpr int kScaleAliasWords = 36;  // TH 64: LDS row stride (dwords), the widest fast window
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
 
@@ -46,7 +52,8 @@ struct ScaleGeom {
   int npv;                       // coefficient pairs per output row (vtaps/2 + 1)
   int range;                     // 0 none, 1 luma tv->pc, 2 chroma tv->pc
   int lds_pairs;                 // max row pairs any tile needs
-  int lds_win_words;             // max source-window dwords any tile needs
+  int lds_win_words;             // max source-window dwords any tile needs (TH 64: rows at
+                                 // kScaleAliasWords, the pair image inside it)
 };
 
 __device__ __forceinline__ int sws_range(int v, int range) {
@@ -96,8 +103,9 @@ __device__ __forceinline__ int hscale_lds(const uint32_t *row, int off, const in
 
 typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 
-// HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio)
-template <int HT, int NPV, bool D4, int RANGE>  // RANGE: g.range as a compile-time value
+// HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio); TH: tile
+// height (64 only with HT 8, NPV 5)
+template <int HT, int NPV, bool D4, int RANGE, int TH>  // RANGE: g.range as a compile-time value
 __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
                                                uint8_t *__restrict__ dst, ScaleGeom g,
                                                const int32_t *__restrict__ hcp,   // [dw][htaps/2]
@@ -106,12 +114,15 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
                                                const int32_t *__restrict__ vps,   // [dh] pair start
                                                const int32_t *__restrict__ hsum) {  // D4: [dw] sum of taps
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  constexpr int LPW = scale_loads_per_wave(TH);
+  constexpr bool ALIAS = TH == 64;
+  static_assert(!ALIAS || (HT == 8 && NPV == 5), "64-row tiles: 2:1 filters only");
   // wave index as a uniform value: the v-pass rows (and their filter rows) are wave-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * kScaleTileH, f = blockIdx.z;
+  const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
   const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off;
   uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off;
-  const int xe = min(x0 + kScaleTileW, g.dw), ye = min(y0 + kScaleTileH, g.dh);
+  const int xe = min(x0 + kScaleTileW, g.dw), ye = min(y0 + TH, g.dh);
   const int p0 = vps[y0], p1 = vps[ye - 1] + g.npv;  // row pairs [p0, p1)
   const int nrows = 2 * (p1 - p0);
   const int npv = NPV ? NPV : g.npv;
@@ -120,20 +131,23 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   const int cb = hp[x0] & ~3;
   // +1: the funnel shift reads one past; rows padded to whole 16-byte pieces
   const int nw = ((((hp[xe - 1] + g.htaps - cb + 3) >> 2) + 1) + 3) & ~3;
-  uint32_t *win = smem;                                       // [nrows][nw]
-  uint32_t *pairs = smem + g.lds_win_words;                   // [p1 - p0][64]
-  uint32_t *vtab = pairs + g.lds_pairs * kScaleTileW;         // [ye - y0][1 + npv]: pair start, coefficients
-  const bool fast = nw <= 36 && nrows <= 4 * kScaleLoadsPerWave * kScaleLoadRows && g.sw >= 16;
+  const int rs = ALIAS ? kScaleAliasWords : nw;  // LDS row stride (dwords)
+  uint32_t *win = smem;                                       // [nrows][rs]
+  // [p1 - p0][ps]: ALIAS, pair p over window rows 2p, 2p+1; else after the window
+  const int ps = ALIAS ? 2 * rs : 64;
+  uint32_t *pairs = ALIAS ? smem : smem + g.lds_win_words;
+  uint32_t *vtab = smem + g.lds_win_words + (ALIAS ? 0 : g.lds_pairs * kScaleTileW);  // [ye - y0][1 + npv]
+  const bool fast = nw <= 36 && nrows <= 4 * LPW * kScaleLoadRows && g.sw >= 16;
   // Every global load of the tile is issued before any is waited on: the window rows, this
   // lane's h filter (column x), and the tile's v filter rows (one entry per thread).
   // fast path: 16-byte pieces, 7 rows of 9 pieces per wave-instruction, 3 per wave (84 rows
   // of <= 144 bytes)
-  u32x4 v[kScaleLoadsPerWave];
+  u32x4 v[LPW];
   const int rr = lane / 9, pc = lane - 9 * rr, col = cb + 16 * pc;
   if (fast) {
 #pragma unroll
-    for (int i = 0; i < kScaleLoadsPerWave; i++) {
-      const int r = kScaleLoadRows * (kScaleLoadsPerWave * wave + i) + rr;
+    for (int i = 0; i < LPW; i++) {
+      const int r = kScaleLoadRows * (LPW * wave + i) + rr;
       const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
       if (col + 16 <= g.sw) {
         v[i] = *(const u32x4_a4 *)(rp + col);
@@ -165,20 +179,20 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   }
   if (fast) {
 #pragma unroll
-    for (int i = 0; i < kScaleLoadsPerWave; i++) {
-      const int r = kScaleLoadRows * (kScaleLoadsPerWave * wave + i) + rr;
+    for (int i = 0; i < LPW; i++) {
+      const int r = kScaleLoadRows * (LPW * wave + i) + rr;
       const u32x4 w = D4 ? v[i] ^ 0x80808080u : v[i];
-      if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw) *(u32x4 *)(win + r * nw + 4 * pc) = w;
+      if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw) *(u32x4 *)(win + r * rs + 4 * pc) = w;
     }
   } else {
     for (int i = tid; i < nrows * nw; i += 256) {
-      const int r = i / nw, c = i - r * nw;
+      const int r = i / nw, c = i - r * nw;  // (LDS word r * rs + c)
       const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
       const int cc = cb + 4 * c;
       uint32_t w = 0;
       for (int bb = 0; bb < 4; bb++)
         if (cc + bb < g.sw) w |= (uint32_t)rp[cc + bb] << (8 * bb);
-      win[i] = w ^ (D4 ? 0x80808080u : 0u);
+      win[r * rs + c] = w ^ (D4 ? 0x80808080u : 0u);
     }
   }
 #pragma unroll 1
@@ -195,23 +209,23 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   for (int p = wave; p < p1 - p0; p += 4) {
     int a, b;
     if (HT || g.htaps <= 16) {
-      a = hscale_lds<HT, D4>(win + (2 * p) * nw, off, hreg, g.htaps, RANGE, hs);
-      b = hscale_lds<HT, D4>(win + (2 * p + 1) * nw, off, hreg, g.htaps, RANGE, hs);
+      a = hscale_lds<HT, D4>(win + (2 * p) * rs, off, hreg, g.htaps, RANGE, hs);
+      b = hscale_lds<HT, D4>(win + (2 * p + 1) * rs, off, hreg, g.htaps, RANGE, hs);
     } else {
-      a = hscale_lds<0, D4>(win + (2 * p) * nw, off, hc, g.htaps, RANGE, hs);
-      b = hscale_lds<0, D4>(win + (2 * p + 1) * nw, off, hc, g.htaps, RANGE, hs);
+      a = hscale_lds<0, D4>(win + (2 * p) * rs, off, hc, g.htaps, RANGE, hs);
+      b = hscale_lds<0, D4>(win + (2 * p + 1) * rs, off, hc, g.htaps, RANGE, hs);
     }
-    pairs[p * 64 + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
+    pairs[p * ps + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
   }
   __syncthreads();
   if (x0 + lane >= g.dw) return;
   for (int y = y0 + wave; y < ye; y += 4) {
     const uint32_t *vr = vtab + (y - y0) * (npv + 1);  // uniform address: LDS broadcast
-    const uint32_t *cp = pairs + ((int)vr[0] - p0) * 64 + lane;
+    const uint32_t *cp = pairs + ((int)vr[0] - p0) * ps + lane;
     int acc = 64 << 12;
 #pragma unroll
     for (int k = 0; k < npv; k++)
-      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, cp[k * 64]),
+      acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, cp[k * ps]),
                                    __builtin_bit_cast(short2_t, vr[1 + k]), acc, false);
     d[(size_t)y * g.d_stride + x0 + lane] = (uint8_t)min(max(acc >> 19, 0), 255);
   }
