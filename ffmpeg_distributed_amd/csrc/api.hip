@@ -356,8 +356,9 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
     const int xe = std::min(x0 + kScaleTileW, dw), cb = p.hf.pos[x0] & ~3;
     max_nw = std::max(max_nw, ((((p.hf.pos[xe - 1] + ht - cb + 3) >> 2) + 1) + 3) & ~3);
   }
+  const int th2 = 64;  // tile height for the 2:1 filters
   const int th = (ht == 8 && npv == 5 && max_nw <= kScaleAliasWords && sw >= 16 &&
-                  2 * tile_pairs(64) <= 4 * scale_loads_per_wave(64) * kScaleLoadRows) ? 64 : 32;
+                  2 * tile_pairs(th2) <= scale_waves(th2) * scale_loads_per_wave(th2) * kScaleLoadRows) ? th2 : 32;
   const int max_pairs = tile_pairs(th);
   p.th = th;
   ScaleGeom &g = p.g;
@@ -365,9 +366,9 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   g.vtaps = vt;
   g.npv = npv;
   g.lds_pairs = max_pairs;
-  if (th == 64) {  // pair image over the window rows (scale.hip: ALIAS)
+  if (th >= 64) {  // pair image over the window rows (scale.hip: ALIAS)
     g.lds_win_words = 2 * max_pairs * kScaleAliasWords;
-    p.lds = ((size_t)g.lds_win_words + (size_t)th * (npv + 1)) * 4;
+    p.lds = (size_t)g.lds_win_words * 4;  // v filter rows by scalar loads
   } else {
     g.lds_win_words = 2 * max_pairs * max_nw;
     p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW + (size_t)th * (npv + 1)) * 4;
@@ -942,13 +943,13 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
 #define MJG_SCALE_LAUNCH3(HT, NPV, D4, TH)                                                          \
   do {                                                                                              \
     if (sg.range == 1)                                                                              \
-      k_scale<HT, NPV, D4, 1, TH><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+      k_scale<HT, NPV, D4, 1, TH><<<grid, 64 * scale_waves(TH), ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
     else if (sg.range == 2)                                                                         \
-      k_scale<HT, NPV, D4, 2, TH><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+      k_scale<HT, NPV, D4, 2, TH><<<grid, 64 * scale_waves(TH), ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
     else                                                                                            \
-      k_scale<HT, NPV, D4, 0, TH><<<grid, 256, ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+      k_scale<HT, NPV, D4, 0, TH><<<grid, 64 * scale_waves(TH), ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
   } while (0)
 #define MJG_SCALE_LAUNCH(HT, NPV, TH)      \
@@ -958,7 +959,9 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     else                                   \
       MJG_SCALE_LAUNCH3(HT, NPV, false, TH); \
   } while (0)
-      if (sg.htaps == 8 && sg.npv == 5 && ps.th == 64)  // 2:1 downscale (4K -> 1080p), 64-row tiles
+      if (sg.htaps == 8 && sg.npv == 5 && ps.th == 128)  // 2:1 downscale (4K -> 1080p), tall tiles
+        MJG_SCALE_LAUNCH(8, 5, 128);
+      else if (sg.htaps == 8 && sg.npv == 5 && ps.th == 64)
         MJG_SCALE_LAUNCH(8, 5, 64);
       else if (sg.htaps == 8 && sg.npv == 5)
         MJG_SCALE_LAUNCH(8, 5, 32);

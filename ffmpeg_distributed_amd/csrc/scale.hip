@@ -38,7 +38,9 @@ typedef short short2_t __attribute__((ext_vector_type(2)));
 
 constexpr int kScaleTileW = 64;
 constexpr int kScaleLoadRows = 7;  // fast window path: rows x 9 pieces per wave-instruction
-__host__ __device__ constexpr int scale_loads_per_wave(int th) { return th == 64 ? 5 : 3; }
+__host__ __device__ constexpr int scale_loads_per_wave(int th) { return th >= 64 ? 5 : 3; }
+// waves per workgroup for a tile height (128-row tiles: 8 waves, 512 threads)
+__host__ __device__ constexpr int scale_waves(int th) { return th == 128 ? 8 : 4; }
 constexpr int kScaleAliasWords = 36;  // TH 64: LDS row stride (dwords), the widest fast window
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
@@ -106,7 +108,7 @@ typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 // HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio); TH: tile
 // height (64 only with HT 8, NPV 5)
 template <int HT, int NPV, bool D4, int RANGE, int TH>  // RANGE: g.range as a compile-time value
-__global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *__restrict__ src,
                                                uint8_t *__restrict__ dst, ScaleGeom g,
                                                const int32_t *__restrict__ hcp,   // [dw][htaps/2]
                                                const int32_t *__restrict__ hp,    // [dw]
@@ -114,9 +116,9 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
                                                const int32_t *__restrict__ vps,   // [dh] pair start
                                                const int32_t *__restrict__ hsum) {  // D4: [dw] sum of taps
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  constexpr int LPW = scale_loads_per_wave(TH);
-  constexpr bool ALIAS = TH == 64;
-  static_assert(!ALIAS || (HT == 8 && NPV == 5), "64-row tiles: 2:1 filters only");
+  constexpr int LPW = scale_loads_per_wave(TH), NWV = scale_waves(TH), NT = 64 * NWV;
+  constexpr bool ALIAS = TH >= 64;
+  static_assert(!ALIAS || (HT == 8 && NPV == 5), "64/128-row tiles: 2:1 filters only");
   // wave index as a uniform value: the v-pass rows (and their filter rows) are wave-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
@@ -136,8 +138,8 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   // [p1 - p0][ps]: ALIAS, pair p over window rows 2p, 2p+1; else after the window
   const int ps = ALIAS ? 2 * rs : 64;
   uint32_t *pairs = ALIAS ? smem : smem + g.lds_win_words;
-  uint32_t *vtab = smem + g.lds_win_words + (ALIAS ? 0 : g.lds_pairs * kScaleTileW);  // [ye - y0][1 + npv]
-  const bool fast = nw <= 36 && nrows <= 4 * LPW * kScaleLoadRows && g.sw >= 16;
+  uint32_t *vtab = smem + g.lds_win_words + g.lds_pairs * kScaleTileW;  // !ALIAS: [ye - y0][1 + npv]
+  const bool fast = nw <= 36 && nrows <= NWV * LPW * kScaleLoadRows && g.sw >= 16;
   // Every global load of the tile is issued before any is waited on: the window rows, this
   // lane's h filter (column x), and the tile's v filter rows (one entry per thread).
   // fast path: 16-byte pieces, 7 rows of 9 pieces per wave-instruction, 3 per wave (84 rows
@@ -170,7 +172,9 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   for (int k = 0; k < (HT ? HT / 2 : 8); k++) hreg[k] = (2 * k < g.htaps) ? hc[k] : 0;
   const int hpx = hp[x];
   const int hs = D4 ? hsum[x] : 0;
-  const int nvt = (ye - y0) * (npv + 1);
+  // v filter rows staged in LDS (ALIAS: read per output row with scalar loads instead -- the
+  // row is wave-uniform -- so the tile's LDS is the window alone: 8 workgroups per CU)
+  const int nvt = ALIAS ? 0 : (ye - y0) * (npv + 1);
   uint32_t vt = 0;
   int vi = tid;
   if (vi < nvt) {
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
       if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw) *(u32x4 *)(win + r * rs + 4 * pc) = w;
     }
   } else {
-    for (int i = tid; i < nrows * nw; i += 256) {
+    for (int i = tid; i < nrows * nw; i += NT) {
       const int r = i / nw, c = i - r * nw;  // (LDS word r * rs + c)
       const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
       const int cc = cb + 4 * c;
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
     }
   }
 #pragma unroll 1
-  for (; vi < nvt; vi += 256) {  // (one pass unless npv > 7)
+  for (; vi < nvt; vi += NT) {  // (one pass unless npv > 7)
     if (vi != tid) {
       const int yy = vi / (npv + 1), k = vi - yy * (npv + 1);
       vt = k == 0 ? (uint32_t)vps[y0 + yy] : (uint32_t)vcp[(size_t)(y0 + yy) * g.npv + (k - 1)];
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   const int off = hpx - cb;
   __syncthreads();
 #pragma unroll 2
-  for (int p = wave; p < p1 - p0; p += 4) {
+  for (int p = wave; p < p1 - p0; p += NWV) {
     int a, b;
     if (HT || g.htaps <= 16) {
       a = hscale_lds<HT, D4>(win + (2 * p) * rs, off, hreg, g.htaps, RANGE, hs);
@@ -219,14 +223,15 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ src,
   }
   __syncthreads();
   if (x0 + lane >= g.dw) return;
-  for (int y = y0 + wave; y < ye; y += 4) {
+  for (int y = y0 + wave; y < ye; y += NWV) {
     const uint32_t *vr = vtab + (y - y0) * (npv + 1);  // uniform address: LDS broadcast
-    const uint32_t *cp = pairs + ((int)vr[0] - p0) * ps + lane;
+    const int32_t *vg = vcp + (size_t)y * npv;         // ALIAS: uniform address: scalar loads
+    const uint32_t *cp = pairs + ((ALIAS ? vps[y] : (int)vr[0]) - p0) * ps + lane;
     int acc = 64 << 12;
 #pragma unroll
     for (int k = 0; k < npv; k++)
       acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, cp[k * ps]),
-                                   __builtin_bit_cast(short2_t, vr[1 + k]), acc, false);
+                                   __builtin_bit_cast(short2_t, ALIAS ? (uint32_t)vg[k] : vr[1 + k]), acc, false);
     d[(size_t)y * g.d_stride + x0 + lane] = (uint8_t)min(max(acc >> 19, 0), 255);
   }
 }
