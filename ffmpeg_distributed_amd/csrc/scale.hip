@@ -139,7 +139,12 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
   const int ps = ALIAS ? 2 * rs : 64;
   uint32_t *pairs = ALIAS ? smem : smem + g.lds_win_words;
   uint32_t *vtab = smem + g.lds_win_words + g.lds_pairs * kScaleTileW;  // !ALIAS: [ye - y0][1 + npv]
-  const bool fast = nw <= 36 && nrows <= NWV * LPW * kScaleLoadRows && g.sw >= 16;
+  // ALIAS: wave w owns the row pairs [w ppw, (w + 1) ppw) of the window: it loads their rows
+  // itself and runs their h-pass with no workgroup barrier in between (its own LDS stores and
+  // loads are ordered), so the waves of a tile start computing as their own rows land
+  const int np = p1 - p0, ppw = ALIAS ? (np + NWV - 1) / NWV : 0;
+  const bool fast = nw <= 36 && g.sw >= 16 &&
+                    (ALIAS ? 2 * ppw <= LPW * kScaleLoadRows : nrows <= NWV * LPW * kScaleLoadRows);
   // Every global load of the tile is issued before any is waited on: the window rows, this
   // lane's h filter (column x), and the tile's v filter rows (one entry per thread).
   // fast path: 16-byte pieces, 7 rows of 9 pieces per wave-instruction, 3 per wave (84 rows
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
   if (fast) {
 #pragma unroll
     for (int i = 0; i < LPW; i++) {
-      const int r = kScaleLoadRows * (LPW * wave + i) + rr;
+      const int r = ALIAS ? 2 * ppw * wave + kScaleLoadRows * i + rr : kScaleLoadRows * (LPW * wave + i) + rr;
       const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
       if (col + 16 <= g.sw) {
         v[i] = *(const u32x4_a4 *)(rp + col);
@@ -184,9 +189,11 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
   if (fast) {
 #pragma unroll
     for (int i = 0; i < LPW; i++) {
-      const int r = kScaleLoadRows * (LPW * wave + i) + rr;
+      const int r = ALIAS ? 2 * ppw * wave + kScaleLoadRows * i + rr : kScaleLoadRows * (LPW * wave + i) + rr;
       const u32x4 w = D4 ? v[i] ^ 0x80808080u : v[i];
-      if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw) *(u32x4 *)(win + r * rs + 4 * pc) = w;
+      // (ALIAS: only this wave's rows -- a neighbour may already have its pairs over its own)
+      if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw && (!ALIAS || kScaleLoadRows * i + rr < 2 * ppw))
+        *(u32x4 *)(win + r * rs + 4 * pc) = w;
     }
   } else {
     for (int i = tid; i < nrows * nw; i += NT) {
@@ -208,9 +215,10 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
     vtab[vi] = vt;
   }
   const int off = hpx - cb;
-  __syncthreads();
+  if (!(ALIAS && fast)) __syncthreads();  // (uniform: the tile's geometry)
+  const int pb = ALIAS ? ppw * wave : wave, pe = ALIAS ? min(pb + ppw, np) : np, pstep = ALIAS ? 1 : NWV;
 #pragma unroll 2
-  for (int p = wave; p < p1 - p0; p += NWV) {
+  for (int p = pb; p < pe; p += pstep) {
     int a, b;
     if (HT || g.htaps <= 16) {
       a = hscale_lds<HT, D4>(win + (2 * p) * rs, off, hreg, g.htaps, RANGE, hs);
