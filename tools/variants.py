@@ -75,8 +75,9 @@ def main():
     for n, rows in res.items():
         enc = sorted(r["encode"] + r["scale"] + r["huff"] for r in rows)
         tot = sorted(sum(r.values()) for r in rows)
+        sc = sorted(r["scale"] for r in rows)
         print(f"{n:12s} scale+huff+encode median {enc[len(enc)//2]:.4f} ms (min {enc[0]:.4f}); "
-              f"all kernels median {tot[len(tot)//2]:.4f} ms per {N} frames")
+              f"all kernels median {tot[len(tot)//2]:.4f} ms per {N} frames; scale alone median {sc[len(sc)//2]:.4f}")
 
 
 if __name__ == "__main__":
