@@ -928,18 +928,24 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (c->scale && !c->fused) {
     tmark(c, S, MJG_K_SCALE, 0);
     const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
-    for (int p = 0; p < 3; p++) {
+    // luma, then U and V in one launch (same filters; blockIdx.z >= n is V) while 2n fits the
+    // grid's z range, else one launch each
+    const bool uv1 = 2 * n <= 65535;
+    for (int p = 0; p < (uv1 ? 2 : 3); p++) {
       PlaneScale &ps = c->ps[p ? 1 : 0];
       ScaleGeom sg = p ? cg : lg;
+      sg.nf = n;
+      sg.s_off = sg.d_off = sg.s_poff = sg.d_poff = 0;
       if (p) {
         sg.s_off = (long long)c->cfg.src_w * c->cfg.src_h + (p - 1) * (long long)cg.sw * cg.sh;
         sg.d_off = g.u_off + (p - 1) * (long long)g.cw * g.ch;
-      } else {
-        sg.s_off = 0;
-        sg.d_off = 0;
+        if (uv1) {
+          sg.s_poff = (long long)cg.sw * cg.sh;
+          sg.d_poff = (long long)g.cw * g.ch;
+        }
       }
       dim3 grid = ps.grid;
-      grid.z = n;
+      grid.z = p && uv1 ? 2 * n : n;
 #define MJG_SCALE_LAUNCH3(HT, NPV, D4, TH)                                                          \
   do {                                                                                              \
     if (sg.range == 1)                                                                              \

@@ -50,6 +50,8 @@ struct ScaleGeom {
   int s_stride, d_stride;
   long long s_off, d_off;        // plane offset inside a frame
   long long s_fstride, d_fstride;  // frame strides
+  int nf;                        // frames per plane: blockIdx.z >= nf is the next plane (U, V in one launch)
+  long long s_poff, d_poff;      // that plane's offset from this one
   int htaps, vtaps;              // htaps multiple of 4 (filterAlign 4), vtaps even
   int npv;                       // coefficient pairs per output row (vtaps/2 + 1)
   int range;                     // 0 none, 1 luma tv->pc, 2 chroma tv->pc
@@ -121,9 +123,10 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
   static_assert(!ALIAS || (HT == 8 && NPV == 5), "64/128-row tiles: 2:1 filters only");
   // wave index as a uniform value: the v-pass rows (and their filter rows) are wave-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * TH, f = blockIdx.z;
-  const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off;
-  uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off;
+  const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * TH, z = blockIdx.z;
+  const int pl = z >= g.nf, f = z - (pl ? g.nf : 0);
+  const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off + (pl ? g.s_poff : 0);
+  uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off + (pl ? g.d_poff : 0);
   const int xe = min(x0 + kScaleTileW, g.dw), ye = min(y0 + TH, g.dh);
   const int p0 = vps[y0], p1 = vps[ye - 1] + g.npv;  // row pairs [p0, p1)
   const int nrows = 2 * (p1 - p0);
