@@ -123,7 +123,20 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
   static_assert(!ALIAS || (HT == 8 && NPV == 5), "64/128-row tiles: 2:1 filters only");
   // wave index as a uniform value: the v-pass rows (and their filter rows) are wave-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int x0 = blockIdx.x * kScaleTileW, y0 = blockIdx.y * TH, z = blockIdx.z;
+  int bx = blockIdx.x, by = blockIdx.y, z = blockIdx.z;
+  if (ALIAS) {
+    // XCD-contiguous tile order: workgroup i runs on XCD i % 8 (round-robin dispatch), so XCD
+    // j takes the j-th eighth of the tiles in raster order and horizontally adjacent tiles --
+    // whose windows share the 128-byte lines at their edges -- meet in the same L2
+    const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+    const int i = bx + gx * (by + gy * z), j = i & 7, q = n >> 3, r = n & 7;
+    const int t = j * q + min(j, r) + (i >> 3);
+    z = t / (gx * gy);
+    const int rem = t - z * gx * gy;
+    by = rem / gx;
+    bx = rem - by * gx;
+  }
+  const int x0 = bx * kScaleTileW, y0 = by * TH;
   const int pl = z >= g.nf, f = z - (pl ? g.nf : 0);
   const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off + (pl ? g.s_poff : 0);
   uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off + (pl ? g.d_poff : 0);
