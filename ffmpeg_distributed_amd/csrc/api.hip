@@ -399,9 +399,9 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
       (rc = dmalloc(&S.d_group_ff, B * NC)) || (rc = dmalloc(&S.d_ff_off, B * NC)) ||
       (rc = dmalloc(&S.d_frame_bits, B * NS)) || (rc = dmalloc(&S.d_status, 4)) ||
       (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)) ||
-      (rc = dmalloc(&S.d_work, 1)))
+      (rc = dmalloc(&S.d_work, (size_t)kXcds * kCtrStride)))
     return rc;
-  HIP_TRY(hipMemset(S.d_work, 0, sizeof(uint32_t)));
+  HIP_TRY(hipMemset(S.d_work, 0, (size_t)kXcds * kCtrStride * sizeof(uint32_t)));
   if (c->rst && ((rc = dmalloc(&S.d_seg_size, B * NS)) || (rc = dmalloc(&S.d_seg_off, B * NS)))) return rc;
   S.out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096 + 2 * NS);
   if ((rc = dmalloc(&S.d_out, S.out_cap))) return rc;
@@ -992,7 +992,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
       launch_fused<kCount>(c, S, src, n);
     else
       launch_encode<kCount>(c, S, enc_in, wgs, ntasks);
-    HIP_TRY(hipMemsetAsync(S.d_work, 0, 4, c->stream));  // batch counter for pass 2
+    HIP_TRY(hipMemsetAsync(S.d_work, 0, (size_t)kXcds * kCtrStride * 4, c->stream));  // unit counters for pass 2
     k_huff_build<<<n * 4, 64, 0, c->stream>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
     tmark(c, S, MJG_K_HUFF, 1);
     HIP_TRY(hipGetLastError());

@@ -1016,6 +1016,28 @@ __device__ __forceinline__ uint64_t dct_mfma(const uint64_t (&raw)[8], int tab, 
   return (((uint64_t)w1 << 32) | w0) & ~1ull;
 }
 
+// k_encode's work units per XCD: workgroup i runs on XCD i % 8 (round-robin dispatch), and
+// XCD j's waves take the units of the j-th eighth of the launch first (its own counter,
+// work_ctr[j * kCtrStride]: neighbouring chunks share the 64-byte sectors at their edges, so
+// they meet in one L2), then the other eighths' leftovers.  Correct for any placement.
+constexpr int kXcds = 8, kCtrStride = 32;  // one 128-byte line per counter
+struct XcdUnits {
+  int j, nbatch;
+  __device__ __forceinline__ int start(int x) const { return (int)(((long long)x * nbatch) / kXcds); }
+  __device__ __forceinline__ int nw(int x, int nwg) const {  // waves of XCD x
+    return ((nwg - x + kXcds - 1) / kXcds) * kWavesPerWg;
+  }
+  // lane 0: the next unit (>= nbatch: none left)
+  __device__ __forceinline__ int next(uint32_t *ctr, int nwg) const {
+    for (int k = 0; k < kXcds; k++) {
+      const int x = (j + k) & (kXcds - 1), e = start(x + 1);
+      const int u = start(x) + nw(x, nwg) + (int)atomicAdd(ctr + x * kCtrStride, 1u);
+      if (u < e) return u;
+    }
+    return nbatch;
+  }
+};
+
 // MF: the DCT stage on the matrix cores (dct_mfma) instead of row_pass + column_screen.
 template <bool RC, int MODE, bool MF = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
@@ -1071,18 +1093,25 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   int aux_frame = -1;  // frame whose histogram / tables s_aux holds (wave-uniform)
   __syncthreads();  // tables visible; the only workgroup barrier
 
-  const int nwaves = gridDim.x * kWavesPerWg;
   const int gw = blockIdx.x * kWavesPerWg + wave;
   constexpr int kBatch = kBatchOf<MF>;
   const int nbatch = (ntasks + kBatch - 1) / kBatch;
-  if (gw >= nbatch) return;
+  const XcdUnits xu{(int)(blockIdx.x & (kXcds - 1)), nbatch};
+  const int nwg = gridDim.x;
+  int u0 = xu.start(xu.j) + (int)(blockIdx.x / kXcds) * kWavesPerWg + wave;  // static first unit
+  if (u0 >= xu.start(xu.j + 1)) {  // none: straight to the counters
+    int v = 0;
+    if (lane == 0) v = xu.next(work_ctr, nwg);
+    u0 = __builtin_amdgcn_readfirstlane(v);
+    if (u0 >= nbatch) return;
+  }
   const int nblk = g.seg_blocks;  // blocks of one entropy-coded segment
   constexpr bool rc = RC;
 
   // Units of kBatch consecutive chunks: the first one static (unit gw), the rest
   // pulled from work_ctr (zeroed by k_scan_bits after every launch), so waves whose
   // picture content is cheap take more batches and all waves finish together.
-  int t = gw * kBatch, tend = min(t + kBatch, ntasks);
+  int t = u0 * kBatch, tend = min(t + kBatch, ntasks);
   uint32_t nb = 0;  // lane 0: the unit after this one
   int frame, chunk, bbase;
   task_pos(g, t, frame, chunk, bbase);
@@ -1097,7 +1126,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     // the next unit is reserved at the top of this unit's last chunk (its rows are prefetched
     // midway through it), not when this unit starts: a wave holding a reserved unit while the
     // counter runs dry left the others idle for up to a whole unit at the end of every launch
-    if (t + 1 == tend && lane == 0) nb = (uint32_t)nwaves + atomicAdd(work_ctr, 1u);
+    if (t + 1 == tend && lane == 0) nb = (uint32_t)xu.next(work_ctr, nwg);
     const uint32_t dsc = s_desc[block_in_mcu(g, b)];
     const int tab = desc_tab(dsc);
     if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, bbase + b, s_desc));
@@ -1541,10 +1570,8 @@ __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk
                                                     uint32_t *__restrict__ work_ctr,
                                                     uint32_t *__restrict__ status) {
   const int f = blockIdx.x;
-  if (f == 0 && threadIdx.x == 0) {
-    *work_ctr = 0;  // k_encode's batch counter, for the next launch
-    *status = 0;    // output overflow flag, set by k_frame_hdr
-  }
+  if (f == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;  // k_encode's unit counters
+  if (f == 0 && threadIdx.x == 0) *status = 0;  // output overflow flag, set by k_frame_hdr
   uint32_t *cb = chunk_bits + (size_t)f * nchunks;
   for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
   __syncthreads();
@@ -1572,10 +1599,8 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
                                                        int nsegs, uint32_t *__restrict__ work_ctr,
                                                        uint32_t *__restrict__ status) {
   const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *work_ctr = 0;
-    *status = 0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *status = 0;
   if (sg >= nsegs) return;
   uint32_t *cb = chunk_bits + (size_t)sg * nchunks;
   for (int i = lane; i < nchunks; i += 64) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
