@@ -549,10 +549,11 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
-// chunks per work unit pulled from the counter: 16 for the VALU DCT stage, 8 for the MFMA stage
-// (3 waves per SIMD, fewer chunks per wave), each the faster on its BASELINE configs
+// chunks per work unit pulled from the counters: 12 for the VALU DCT stage (with the per-XCD
+// counters: c2 -6%, c5 -5% against 16; 8 and 24 measured too), 8 for the MFMA stage (3 waves
+// per SIMD, fewer chunks per wave), each the faster on its BASELINE configs
 template <bool MF>
-constexpr int kBatchOf = MF ? 8 : 16;
+constexpr int kBatchOf = MF ? 8 : 12;
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
 // quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
