@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=4.0,
                    help="CPU baseline: wall seconds per point of the core-count sweep")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (rank 0, N=1 only)")
+    p.add_argument("--e2e-segments", type=int, default=6)
     p.add_argument("--fused", action="store_true",
                    help="-vf scale configs: the opt-in fused k_scale_encode instead of k_scale + k_encode")
     p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
@@ -158,6 +160,97 @@ def cpu_baseline(seconds: float):
                       f"path, not FFmpeg's SIMD encoder: FFmpeg is absent on this pool), one frame "
                       f"per process at a time",
             "host": hc, "sweep": sweep}
+
+
+# ------------------------------------------------------------------------ end to end
+E2E_ARGS = {  # remote_args of each workload (fd.py:190 splits them from the CLI string)
+    "c2": "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
+    "c1": "-c:v mjpeg -q:v 5 -dct int -bitexact",
+    "c4": "-vf scale=1920:1080:flags=bicubic -c:v mjpeg -q:v 3 -dct int -huffman default -bitexact",
+    "c5": "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact",
+}
+
+
+def e2e(workload: str, device: int, segments: int, tmpdir=None):
+    """End-to-end frames/s through the reference's worker contract (fd.py:131-141: segment
+    file on stdin, Matroska on stdout, progress on stderr, exit code), timed outside the
+    `value` region: one raw I420 Matroska segment of the workload (page cache) encoded
+    `segments` times by
+      per_segment_process: the dispatcher's TaskThread path for -H gpu:N, one process per
+                           segment (mjg_client -> the resident encoder of the GPU);
+      persistent:          the dispatcher's -P path (one `worker --serve` per host);
+      python_worker:       one `python -m ffmpeg_distributed_amd.worker` process per segment
+                           (MJG_RESIDENT=0; round 2's per-segment path), 2 segments.
+    Steady fps = frames / median seconds of the segments after the first (which starts the
+    resident encoder or the server: reported as first_segment_s)."""
+    import shlex
+    import statistics
+    import subprocess
+    import tempfile
+    from fractions import Fraction
+    from ffmpeg_distributed_amd import dispatcher as D
+    from ffmpeg_distributed_amd.testsrc import write_raw_segment
+    w, h, _, _, _, seg_frames, full, _, _ = WORKLOADS[workload]
+    fps = Fraction(30) if workload == "c1" else Fraction(60) if workload in ("c2", "c4") else Fraction(30)
+    args = shlex.split(E2E_ARGS[workload])
+    d = tempfile.mkdtemp(prefix="mjg_e2e_", dir=tmpdir)
+    seg = os.path.join(d, "seg.mkv")
+    host = f"gpu:{device}"
+    out = {"segment": f"{seg_frames} frames {w}x{h} raw I420 Matroska (V_UNCOMPRESSED), page cache",
+           "remote_args": E2E_ARGS[workload]}
+    try:
+        t = time.monotonic()
+        nbytes = write_raw_segment(seg, w, h, fps, seg_frames, full_range=full)
+        out["segment_bytes"] = nbytes
+        out["segment_write_s"] = round(time.monotonic() - t, 2)
+
+        def leg(run_one, n):
+            secs = []
+            for i in range(n):
+                dst = os.path.join(d, f"out{i % 2}.mkv")
+                t0 = time.monotonic()
+                rc = run_one(dst)
+                secs.append(time.monotonic() - t0)
+                if rc != 0:
+                    raise RuntimeError(f"segment {i} exited {rc}")
+            steady = statistics.median(secs[1:]) if n > 1 else secs[0]
+            return {"segments": n, "first_segment_s": round(secs[0], 4),
+                    "steady_s_per_segment": round(steady, 4), "fps_steady": round(seg_frames / steady, 1),
+                    "seconds": [round(x, 4) for x in secs]}
+
+        def per_process(resident):
+            argv = D.worker_argv(host, args, resident=resident)
+
+            def one(dst):
+                with open(seg, "rb") as fi, open(dst, "wb") as fo:
+                    p = D.FFMPEGProc(argv, stdin=fi, stdout=fo)
+                    rc = p.run()
+                if rc != 0:
+                    sys.stderr.write(p.stderr[-2000:])
+                return rc
+            return one
+
+        if D.resident_enabled():
+            r = leg(per_process(True), segments)
+            r["argv"] = "mjg_client --device N -- <remote_args> (resident encoder per GPU)"
+            out["per_segment_process"] = r
+            subprocess.run([D.CLIENT, "--device", str(device), "--shutdown"], timeout=60)
+        srv = D.GpuServer(host)
+        try:
+            r = leg(lambda dst: srv.run_task(D.Task(seg, dst, args)), segments)
+        finally:
+            srv.close()
+        r["argv"] = "python -m ffmpeg_distributed_amd.worker --device N <remote_args> --serve (-P)"
+        out["persistent"] = r
+        r = leg(per_process(False), 2)
+        r["argv"] = "python -m ffmpeg_distributed_amd.worker --device N <remote_args> (MJG_RESIDENT=0)"
+        r["fps_steady"] = round(seg_frames / min(r["seconds"]), 1)
+        out["python_worker"] = r
+    finally:
+        for f in os.listdir(d):
+            os.remove(os.path.join(d, f))
+        os.rmdir(d)
+    return out
 
 
 # ------------------------------------------------------------------------ roofline
@@ -310,6 +403,12 @@ def main():
 
     out = None
     if rank == 0:
+        e2e_res = None
+        if not a.no_e2e and world == 1 and a.content == "testsrc" and not a.rst and not a.fused:
+            try:
+                e2e_res = e2e(a.workload, local, a.e2e_segments)
+            except Exception as e:  # reported, never fatal for the GPU number
+                e2e_res = {"error": repr(e)}
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             try:
@@ -347,6 +446,7 @@ def main():
             "roofline_kernels": per_kernel,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},
             "mean_jpeg_bytes": round(mean_jpeg, 1),
+            "e2e": e2e_res,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -62,7 +62,50 @@ def check() -> bool:
         return f.read().strip() == source_digest()
 
 
+CLIENT = os.path.join(PKG, "mjg_client")
+CLIENT_STAMP = CLIENT + ".sha256"
+CLIENT_SRC = os.path.join(CSRC, "mjg_client.c")
+
+
+def _client_command(out: str):
+    return [os.environ.get("CC", "gcc"), "-O2", "-Wall", "-o", out, CLIENT_SRC]
+
+
+def client_digest() -> str:
+    h = hashlib.sha256()
+    with open(CLIENT_SRC, "rb") as f:
+        h.update(f.read())
+    h.update(" ".join(_client_command("OUT")[1:]).replace(ROOT, "ROOT").encode())
+    return h.hexdigest()
+
+
+def client_check() -> bool:
+    """True when the mjg_client binary exists and was built from the current source."""
+    if not os.path.exists(CLIENT) or not os.path.exists(CLIENT_STAMP):
+        return False
+    with open(CLIENT_STAMP) as f:
+        return f.read().strip() == client_digest()
+
+
+def build_client(force: bool = False, verbose: bool = False) -> str:
+    """The native per-segment client of the resident encoder (csrc/mjg_client.c)."""
+    if not force and client_check():
+        return CLIENT
+    tmp = f"{CLIENT}.tmp{os.getpid()}"
+    cmd = _client_command(tmp)
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, CLIENT)
+    with open(f"{CLIENT_STAMP}.tmp{os.getpid()}", "w") as f:
+        f.write(client_digest() + "\n")
+    os.replace(f"{CLIENT_STAMP}.tmp{os.getpid()}", CLIENT_STAMP)
+    return CLIENT
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    if shutil.which(_client_command("x")[0]) and (force or not client_check()):
+        build_client(force, verbose)
     if not force and check():
         return LIB
     # per-process temporaries and atomic renames: ranks of one node that find the library

@@ -185,10 +185,23 @@ def _report(msg: str):
     (tqdm.write if tqdm else print)(msg, file=sys.stderr)
 
 
-def worker_argv(host: str, ffmpeg_args: List[str]) -> List[str]:
-    """The per-segment worker command for one -H entry (fd.py:131-138 + gpu:N)."""
+CLIENT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mjg_client")
+
+
+def resident_enabled() -> bool:
+    """gpu:N segments go through mjg_client and the resident encoder (resident.py) when the
+    client is built, unless MJG_RESIDENT=0 asks for one Python worker process per segment."""
+    return os.environ.get("MJG_RESIDENT", "1") != "0" and os.access(CLIENT, os.X_OK)
+
+
+def worker_argv(host: str, ffmpeg_args: List[str], resident: Optional[bool] = None) -> List[str]:
+    """The per-segment worker command for one -H entry (fd.py:131-138 + gpu:N).  gpu:N:
+    `mjg_client` (hands the segment to its GPU's resident encoder; the same stdin / stdout /
+    stderr / exit-code contract) or, with resident=False, a `worker` process of its own."""
     g = GPU_HOST.match(host)
     if g:
+        if resident if resident is not None else resident_enabled():
+            return [CLIENT, "--device", g.group(1), "--python", sys.executable, "--", *ffmpeg_args]
         return [sys.executable, "-m", "ffmpeg_distributed_amd.worker", "--device", g.group(1),
                 *ffmpeg_args]
     cmd = ["nice", "-n10", "ionice", "-c3", "ffmpeg", "-f", "matroska", "-i", "pipe:",
@@ -200,7 +213,7 @@ def worker_argv(host: str, ffmpeg_args: List[str]) -> List[str]:
 
 def server_argv(host: str, ffmpeg_args: List[str]) -> List[str]:
     """The persistent worker for a gpu:N host (--persistent-gpu-workers): worker.serve."""
-    return worker_argv(host, ffmpeg_args) + ["--serve"]
+    return worker_argv(host, ffmpeg_args, resident=False) + ["--serve"]
 
 
 SERVE_DONE = "mjg-serve: segment done rc="

@@ -164,3 +164,21 @@ def noise_patches_i420_torch(w: int, h: int, t0: int, n: int, device, full_range
 
 CONTENT = {"testsrc": testsrc2_i420_torch, "natural": natural_i420_torch,
            "noise-patches": noise_patches_i420_torch}
+
+
+def write_raw_segment(path: str, w: int, h: int, fps, frames: int, distinct: int = 8,
+                      full_range: bool = False) -> int:
+    """A raw V_UNCOMPRESSED I420 Matroska segment of `frames` testsrc2-like frames (cycling
+    `distinct` of them), the splitter's `-c copy` of raw video.  Returns
+    its size in bytes."""
+    import os
+    from fractions import Fraction
+    from .container import MkvWriter
+    pool = [testsrc2_i420(w, h, t, full_range=full_range).tobytes() for t in range(min(distinct, max(frames, 1)))]
+    with open(path, "wb") as f:
+        wr = MkvWriter(f, w, h, Fraction(fps), codec="V_UNCOMPRESSED", colour_space=b"I420",
+                       colour_range=2 if full_range else 0)
+        for i in range(frames):
+            wr.write_frame(pool[i % len(pool)])
+        wr.close()
+    return os.path.getsize(path)

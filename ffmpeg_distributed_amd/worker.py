@@ -26,6 +26,7 @@ import sys
 import threading
 import time
 from fractions import Fraction
+from dataclasses import dataclass
 from typing import List, Optional
 
 from . import container, profile
@@ -90,6 +91,33 @@ READ_THREADS = int(os.environ.get("MJG_READ_THREADS", "4"))
 # MJG_WORKER_TRACE=1: one `mjg-trace:` stderr line per segment with where its time went
 # (reader, submit, sync, fetch, mux) and the process's CPU / NUMA placement.
 TRACE = os.environ.get("MJG_WORKER_TRACE", "0") == "1"
+
+
+@dataclass(frozen=True)
+class Options:
+    """Per-segment settings.  A worker process takes them from its environment (the module
+    values above); the resident encoder (resident.py) takes them from each request, i.e. from
+    the environment of the mjg_client process that sent the segment."""
+    batch: int = 0                  # MJG_WORKER_BATCH: frames per submit (0: by bytes)
+    batch_bytes: int = 96 << 20     # MJG_WORKER_BATCH_BYTES
+    com_itu601: bool = False        # MJG_COM_ITU601
+    read_threads: int = 4           # MJG_READ_THREADS
+    trace: bool = False             # MJG_WORKER_TRACE
+
+    @classmethod
+    def from_env(cls, env, batch_bytes: Optional[int] = None) -> "Options":
+        """From NAME=VALUE settings (absent names take the defaults above)."""
+        return cls(batch=int(env.get("MJG_WORKER_BATCH", "0") or 0),
+                   batch_bytes=int(env.get("MJG_WORKER_BATCH_BYTES", "0") or 0) or batch_bytes or (96 << 20),
+                   com_itu601=env.get("MJG_COM_ITU601", "0") == "1",
+                   read_threads=max(1, int(env.get("MJG_READ_THREADS", "4") or 4)),
+                   trace=env.get("MJG_WORKER_TRACE", "0") == "1")
+
+
+def process_options(batch_bytes: Optional[int] = None) -> Options:
+    """This process's settings (the module values, read from its environment at import)."""
+    return Options(batch=BATCH, batch_bytes=batch_bytes or BATCH_BYTES, com_itu601=COM_ITU601,
+                   read_threads=READ_THREADS, trace=TRACE)
 # Bind the worker to its GPU's NUMA node (CPUs, and preferred memory for its page-locked
 # batches), see bind_numa.  MJG_NUMA_BIND=0 leaves placement to the scheduler.
 NUMA_BIND = os.environ.get("MJG_NUMA_BIND", "1") == "1"
@@ -98,12 +126,15 @@ _gpu_node = -1
 
 
 def bind_numa(device: int) -> int:
-    """Run this process's threads from here on on the CPUs of `device`'s NUMA node and
-    prefer that node for its memory: the segment's positional reads copy page-cache pages
-    into page-locked batches that the GPU then reads over PCIe, and both the copy and the
-    DMA cross the socket interconnect when the process sits on the other node.  Threads
-    started later (reader, pread pool) inherit the mask; the process's first allocation of
-    the batches follows the memory policy.  Returns the node (-1: unknown / not bound)."""
+    """Run the calling thread, and the threads it starts from here on, on the CPUs of
+    `device`'s NUMA node and prefer that node for their memory: the segment's positional
+    reads copy page-cache pages into page-locked batches that the GPU then reads over PCIe,
+    and both the copy and the DMA cross the socket interconnect when the process sits on the
+    other node.  Affinity and memory policy are per thread on Linux: threads started later
+    (reader, pread pool) inherit them, threads that already exist (the HIP runtime's, which
+    the NUMA query itself starts) do not.  When the node's CPUs are not among the allowed
+    ones nothing changes (no remote memory preference for a thread that cannot run there).
+    Returns the node (-1: unknown / not bound)."""
     global _bound_node, _gpu_node
     if _bound_node is not None:
         return _bound_node
@@ -118,8 +149,9 @@ def bind_numa(device: int) -> int:
     try:
         with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
             cpus = _cpulist(f.read().strip()) & os.sched_getaffinity(0)
-        if cpus:
-            os.sched_setaffinity(0, cpus)
+        if not cpus:
+            return -1
+        os.sched_setaffinity(0, cpus)
     except OSError:
         return -1
     _prefer_node(node)
@@ -215,7 +247,7 @@ def _pread_exact(fd: int, dest, off: int) -> None:
 class Source:
     """Packed planar frames from stdin: .info (StreamInfo), .read_into(buf, n) -> count."""
 
-    def __init__(self, raw):
+    def __init__(self, raw, read_threads: int = READ_THREADS):
         self.child = None
         self.feeder = None
         head = raw.read(4)
@@ -239,7 +271,7 @@ class Source:
             self._fd = _regular_file_fd(raw)
             if self._fd is not None:  # a file (the dispatcher's segment): parallel positional reads
                 from concurrent.futures import ThreadPoolExecutor
-                self._pool = ThreadPoolExecutor(READ_THREADS)
+                self._pool = ThreadPoolExecutor(read_threads)
                 self.read_into = self._read_mkv_pread
             return
         # any other codec: ffmpeg decodes, we read its y4m
@@ -368,10 +400,12 @@ def ffmpeg_fallthrough(src: Source, args: List[str], stdout) -> int:
 
 
 def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cache=None,
-        batch_bytes: Optional[int] = None) -> int:
-    """One segment, stdin -> stdout.  `cache` (serve mode): a dict that keeps the encoder
-    context and the page-locked batch buffers between segments of the same stream shape."""
+        batch_bytes: Optional[int] = None, opts: Optional[Options] = None) -> int:
+    """One segment, stdin -> stdout.  `cache` (serve / resident mode): a dict that keeps the
+    encoder context and the page-locked batch buffers between segments of the same stream
+    shape.  `opts`: the segment's settings (default: this process's, process_options)."""
     t_run = time.monotonic()
+    opts = opts or process_options(batch_bytes)
     stdin = stdin or sys.stdin.buffer
     stdout = stdout or sys.stdout.buffer
     stderr = stderr or sys.stderr
@@ -381,7 +415,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         stderr.flush()
         return passthrough(args, stdin, stdout)
 
-    src = Source(stdin)
+    src = Source(stdin, opts.read_threads)
     info = src.info
     if prof.chroma is not None and prof.chroma != info.chroma:
         stderr.write(f"gpu:{device}: -pix_fmt needs {info.chroma} -> {prof.chroma} chroma resampling; "
@@ -392,11 +426,11 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     bind_numa(device)  # before the reader threads and the batch buffers
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
-    batch = BATCH or max(1, min(32, (batch_bytes or BATCH_BYTES) // max(info.frame_bytes, 1)))
+    batch = opts.batch or max(1, min(32, opts.batch_bytes // max(info.frame_bytes, 1)))
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     key = (info.width, info.height, dst_w, dst_h, info.full_range, prof.qscale, sar,
-           COM_ITU601 and not info.full_range, prof.huffman, info.chroma, prof.rst, batch)
+           opts.com_itu601 and not info.full_range, prof.huffman, info.chroma, prof.rst, batch)
     nbuf = 3
     if cache is not None and cache.get("key") == key:
         enc, bufs = cache["enc"], cache["bufs"]
@@ -405,7 +439,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
             release(cache)
         enc = MjpegEncoder(device, info.width, info.height, dst_w, dst_h, full_range=info.full_range,
                            qscale=prof.qscale, sar=sar, max_batch=batch,
-                           com_itu601=COM_ITU601 and not info.full_range, huffman=prof.huffman,
+                           com_itu601=opts.com_itu601 and not info.full_range, huffman=prof.huffman,
                            chroma=info.chroma, rst=prof.rst)
         bufs = [PinnedBuffer(batch * enc.frame_bytes) for _ in range(nbuf)]
         if cache is not None:
@@ -455,7 +489,12 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     def muxer():
         nonlocal frames
         while True:
-            item = outq.get()
+            try:
+                item = outq.get(timeout=0.1)
+            except queue.Empty:
+                if abort.is_set():  # error path: the main thread may not be able to post None
+                    return
+                continue
             if item is None:
                 return
             if mux_err:
@@ -516,7 +555,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         mkv.close()
         prog.update(frames, 0, final=True)
         failed = False
-        if TRACE:
+        if opts.trace:
             stderr.write(f"mjg-trace: frames={frames} total={time.monotonic() - t_seg:.4f} "
                          f"setup={t_seg - t_run:.4f} "
                          + " ".join(f"{k}={v:.4f}" for k, v in tr.items()) + f" {placement()}\n")
@@ -529,7 +568,10 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         abort.set()
         free.put(-1)
         if mt.is_alive():  # error path: let the muxer finish what it holds, then stop
-            outq.put(None)
+            try:  # never block here: a full queue means the muxer is inside a write, and it
+                outq.put_nowait(None)  # sees `abort` once that write returns
+            except queue.Full:
+                pass
             mt.join(timeout=5.0)
         th.join(timeout=5.0)
         if th.is_alive():

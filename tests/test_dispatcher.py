@@ -116,7 +116,7 @@ def test_worker_argv():
                                                 "-i", "pipe:", *args, "-f", "matroska", "pipe:"]
     ssh = D.worker_argv("me@box", args)
     assert ssh[:2] == ["ssh", "me@box"] and ssh[2].startswith("nice -n10 ionice -c3 ffmpeg -f matroska")
-    g = D.worker_argv("gpu:3", args)
+    g = D.worker_argv("gpu:3", args, resident=False)
     assert g == [sys.executable, "-m", "ffmpeg_distributed_amd.worker", "--device", "3", *args]
 
 

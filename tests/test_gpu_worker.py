@@ -179,3 +179,36 @@ def test_worker_serve_segment_failing_mid_stream(tmp_path, monkeypatch):
         r = container.MkvReader(io.BytesIO((tmp_path / f"out{i}.mkv").read_bytes()))
         want = [oracle.encode_frame(*split_i420(f, w, h), full_range=False, qscale=q, sar=(1, 1)) for f in frames]
         assert [d for _, d in r.frames(1)] == want, f"segment {i}"
+
+
+def test_resident_client_segments_match_oracle(tmp_path):
+    """The dispatcher's per-segment process for -H gpu:0 is mjg_client, which hands the
+    segment to the GPU's resident encoder (started on first use): every packet equals the
+    oracle's encode, a failing segment exits 1 with its error on stderr, and the next segment
+    of another shape comes out byte-exact too (fd.py:131-141 contract)."""
+    import subprocess
+    import sys
+    from ffmpeg_distributed_amd import build, dispatcher as D
+    client = build.build_client()
+    cases = [(96, 64, 5, 3), (96, 64, 5, 9), (80, 48, 5, 4)]
+    argv = D.worker_argv("gpu:0", _args(5), resident=True)
+    assert argv[0] == client
+    try:
+        for i, (w, h, q, n) in enumerate(cases):
+            frames = [make_testsrc(w, h, 13 * i + k) for k in range(n)]
+            (tmp_path / f"in{i}.mkv").write_bytes(_raw_mkv(frames, w, h))
+            with open(tmp_path / f"in{i}.mkv", "rb") as fi, open(tmp_path / f"out{i}.mkv", "wb") as fo:
+                p = D.FFMPEGProc(argv, stdin=fi, stdout=fo)
+                assert p.run() == 0, p.stderr
+            assert p.duration is not None
+            r = container.MkvReader(io.BytesIO((tmp_path / f"out{i}.mkv").read_bytes()))
+            want = [oracle.encode_frame(*split_i420(f, w, h), full_range=False, qscale=q, sar=(1, 1)) for f in frames]
+            assert [d for _, d in r.frames(1)] == want, f"segment {i}"
+            if i == 0:
+                bad = _raw_mkv([make_testsrc(96, 64, 50 + k) for k in range(4)], 96, 64)
+                (tmp_path / "bad.mkv").write_bytes(bad[: len(bad) - 100])
+                with open(tmp_path / "bad.mkv", "rb") as fi, open(tmp_path / "outbad.mkv", "wb") as fo:
+                    p = D.FFMPEGProc(argv, stdin=fi, stdout=fo)
+                    assert p.run() == 1 and "ends inside a frame" in p.stderr
+    finally:
+        subprocess.run([client, "--device", "0", "--shutdown"], timeout=60)

@@ -90,8 +90,8 @@ def test_dispatcher_spreads_segments_over_gpu_hosts(tmp_path, monkeypatch):
     stub.write_text(STUB_WORKER)
     real = D.worker_argv
 
-    def argv(host, args):
-        a = real(host, args)
+    def argv(host, args, resident=None):
+        a = real(host, args, resident=False)
         assert a[:3] == [sys.executable, "-m", "ffmpeg_distributed_amd.worker"]
         return [sys.executable, str(stub)] + a[3:]
 
@@ -149,8 +149,8 @@ def test_dispatcher_persistent_gpu_workers(tmp_path, monkeypatch):
     stub.write_text(STUB_SERVER)
     real = D.worker_argv
 
-    def argv(host, args):
-        a = real(host, args)
+    def argv(host, args, resident=None):
+        a = real(host, args, resident=False)
         assert a[:3] == [sys.executable, "-m", "ffmpeg_distributed_amd.worker"]
         return [sys.executable, str(stub)] + a[3:]
 
