@@ -68,6 +68,32 @@ def test_profile_qscale_mapping(q, expect):
     assert profile.effective_qscale(q) == expect
 
 
+def test_boundary_flag_substitutions():
+    """The substitutions INTEGRATION.md documents: every accepted -vf scale flag set (plain
+    bicubic, BASELINE's own form; no flags= at all; bicubic+accurate_rnd+bitexact) is encoded
+    by swscale's bitexact + accurate_rnd C path -- the encoder is always opened with
+    sws_bitexact (the worker never passes another value) -- and -q:v goes through
+    update_qscale with the qmin = 2 / qmax = 31 clip."""
+    import inspect
+    from ffmpeg_distributed_amd.encoder import MjpegEncoder
+    base = "-c:v mjpeg -q:v 5 -dct int -huffman default -bitexact"
+    for vf, flags in [("scale=1920:1080:flags=bicubic", ("bicubic",)),
+                      ("scale=1920:1080", ("bicubic",)),
+                      ("scale=w=1920:h=1080:flags=bicubic+accurate_rnd+bitexact",
+                       ("bicubic", "accurate_rnd", "bitexact"))]:
+        p = profile.parse(f"-vf {vf} {base}")
+        assert p.scale == (1920, 1080) and p.sws_flags == flags
+    assert inspect.signature(MjpegEncoder).parameters["sws_bitexact"].default is True
+    with open(os.path.join(ROOT, "ffmpeg_distributed_amd", "worker.py")) as f:
+        assert "sws_bitexact" not in f.read()
+    for vf in ("scale=1920:1080:flags=bilinear", "scale=1920:1080:flags=bicubic+neighbor",
+               "scale=1920:1080:flags=accurate_rnd"):
+        assert profile.try_parse(f"-vf {vf} {base}")[0] is None
+    # q < 2 clips to qmin 2; fractional -q:v truncates lambda first
+    assert [profile.effective_qscale(q) for q in (0.5, 1, 1.9, 2, 2.5, 3, 31, 40)] == [2, 2, 2, 2, 3, 3, 31, 31]
+    assert profile.parse("-c:v mjpeg -q:v 1 -dct int -bitexact").qscale == 2
+
+
 @pytest.mark.parametrize("args", [
     "-c:v libx264 -crf 18",
     "-c:v mjpeg -q:v 5 -dct int -huffman zigzag -bitexact",
