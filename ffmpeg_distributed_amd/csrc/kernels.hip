@@ -9,9 +9,9 @@
 //                 Huffman bit-length pass -> wave prefix-sum -> bit-pack pass into an
 //                 LDS window (ds_or_b32) -> chunk bitstream to a scratch slot
 //   k_scan_bits   per frame: exclusive scan of chunk bit lengths
-//   k_count_ff    per chunk: realign its bits to the frame offset, pad with 1s, count 0xFF
-//   k_scan_ff     per frame: exclusive scan of 0xFF counts -> stuffed frame size
-//   k_write       per chunk: header / stuffed scan bytes / EOI into the packed output
+//   k_stuff       per group of 8 chunks, one pass: realign the bits to the frame offset, pad
+//                 with 1s, count 0xFF, look back for the packed output offset, then header /
+//                 stuffed scan bytes / RSTn / EOI into the packed output
 //
 // Arithmetic follows FFmpeg (see oracle/mjpeg_oracle.c for the per-function citations):
 // libavcodec/jfdctint_template.c, mpegvideo_enc.c dct_quantize_c, mjpegenc.c
@@ -435,60 +435,107 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
 // -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
 // (layout of the table block: AC luma 0-255, AC chroma 256-511, DC luma 512-527,
 // DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.
-// It also records every symbol with its mantissa in the lane's record column (rec[j * 64]:
-// DC flag << 31 | (DC category or AC symbol) << 16 | mantissa), so the emission pass
-// replays the symbols (k_emit_syms) instead of recomputing the block.
-constexpr int kSymCap = 68;  // symbols per block: DC + 63 AC + 3 ZRL + EOB
+// It also records every symbol with its mantissa as a bit stream in the lane's record column
+// (rec[j * 64] = stream word j, MSB first), so the emission pass replays the symbols
+// (k_emit_syms) instead of recomputing the block: the DC as its category (4 bits) and
+// mantissa (category bits), each AC symbol as its (run, size) byte and mantissa (size bits).
+// ~11 bits per symbol instead of a 32-bit record: the count pass writes ~3x fewer bytes and
+// k_emit_syms finds most blocks' streams in the words it prefetched a chunk ahead.
+// symn = records | stream words << 8.
+constexpr int kRecWords = 40;  // >= (15 + 63 * 18 + 4 * 8 + 31) / 32 stream words per block (68 symbols at most)
 struct CountSink {
   uint32_t *hac, *hdc;
   uint32_t *rec;
-  uint32_t n = 0;
+  uint64_t acc = 0;  // pending stream bits in the low nb bits (higher bits: already stored)
+  uint32_t nb = 0, nw = 0, n = 0;  // pending bits (< 32 between pushes), words stored, symbols
+  __device__ __forceinline__ void push(uint32_t v, int len) {
+    acc = (acc << len) | v;
+    nb += (uint32_t)len;
+    if (nb >= 32) {
+      nb -= 32;
+      rec[nw * 64] = (uint32_t)(acc >> nb);
+      nw++;
+    }
+  }
   __device__ __forceinline__ void dc(int cat, uint32_t mant) {
     atomicAdd(&hdc[cat], 1u);
-    rec[n * 64] = (1u << 31) | ((uint32_t)cat << 16) | mant;
+    push(((uint32_t)cat << cat) | mant, 4 + cat);
     n++;
   }
-  __device__ __forceinline__ void ac(int sym, int, uint32_t mant) {
+  __device__ __forceinline__ void ac(int sym, int cat, uint32_t mant) {
     atomicAdd(&hac[sym], 1u);
-    rec[n * 64] = ((uint32_t)sym << 16) | mant;
+    push(((uint32_t)sym << cat) | mant, 8 + cat);
     n++;
   }
-  __device__ __forceinline__ void finish() {}
+  // the last word (left-aligned) and the block's record / word counts
+  __device__ __forceinline__ uint32_t finish() {
+    if (nb) rec[nw * 64] = (uint32_t)(acc << (32 - nb));
+    return n | ((nw + (nb ? 1u : 0u)) << 8);
+  }
 };
 
-// Raw 8x8 block as 8 little-endian row words.  fetch_rows issues the 8-byte row loads
-// for interior blocks (the prefetch path, 16 VGPRs) and returns false for blocks that
-// touch the frame edge or are misaligned; fetch_rows_edge builds those with
-// coordinate clamping (FFmpeg emulated_edge_mc / draw_edges replicate the last
-// row/column) at a point where no other block data is live.
-struct Src {
-  const uint8_t *plane;
+// Raw 8x8 block as 8 little-endian row words.  Addresses are 32-bit offsets from the frame's
+// base, which is wave-uniform (a chunk never spans two frames): the loads take the base from
+// SGPRs and one VGPR offset (global_load saddr form), no 64-bit address arithmetic per row.
+// A block's plane fields come from the block-of-MCU descriptor table in LDS (BlockDesc, one
+// entry per block of the MCU): no per-lane branch on the plane.  fetch_rows issues the 8-byte
+// row loads for interior blocks (the prefetch path, 16 VGPRs) and returns false for blocks that
+// touch the frame edge or are misaligned; fetch_rows_edge builds those with coordinate clamping
+// (FFmpeg emulated_edge_mc / draw_edges replicate the last row/column) at a point where no
+// other block data is live.
+struct BlockDesc {  // LDS, two uint4 per block of the MCU
+  uint32_t poff;    // plane offset in the frame (0, U, V)
+  int stride, pw, ph;
+  int xs, ys, dx, dy;  // x0 = mx * xs + dx, y0 = my * ys + dy
+};
+
+struct BlockPos {
+  uint32_t poff;
   int stride, pw, ph, x0, y0;
 };
 
+// Position of block b (index in the frame's coding order) in its frame.
+__device__ __forceinline__ BlockPos block_pos(const EncGeom &g, int b, const uint4 *s_bd) {
+  // (24-bit multiplies: every operand here is below 2^24)
+  const int m = (int)__umulhi((uint32_t)b, g.bpm_magic);
+  const int i = b - __mul24(m, g.bpm);
+  const int my = g.mbw == 1 ? m : (int)__umulhi((uint32_t)m, g.mbw_magic), mx = m - __mul24(my, g.mbw);
+  const uint4 a = s_bd[2 * i], c = s_bd[2 * i + 1];
+  BlockPos p;
+  p.poff = a.x;
+  p.stride = (int)a.y;
+  p.pw = (int)a.z;
+  p.ph = (int)a.w;
+  p.x0 = __mul24(mx, (int)c.x) + (int)c.z;
+  p.y0 = __mul24(my, (int)c.y) + (int)c.w;
+  return p;
+}
+
 // The block's 8 rows when it is active, inside its plane and 8-byte aligned (returns true);
-// otherwise every row load reads `safe` (the frames' base, aligned and valid) and the caller
+// otherwise every row load reads the frame's first bytes (aligned and valid) and the caller
 // refetches with fetch_rows_edge.  Unconditional loads: no per-lane branch and no zeroing of
-// the row registers around them.
-__device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const Src &s, bool active, const uint8_t *safe) {
-  // row offset y0 * stride < the plane size < 2^32, operands < 2^24
-  const uint8_t *base = s.plane + ((uint32_t)__umul24((uint32_t)s.y0, (uint32_t)s.stride) + (uint32_t)s.x0);
-  const bool fast = active && (s.x0 + 8 <= s.pw) && (s.y0 + 8 <= s.ph) &&
-                    ((((uintptr_t)base) | (uintptr_t)s.stride) & 7) == 0;
-  const uint8_t *p = fast ? base : safe;
-  const size_t st = fast ? (size_t)s.stride : 0;
+// the row registers around them.  fb: the frame's base (wave-uniform, 8-byte aligned when
+// fb_aligned).
+__device__ __forceinline__ bool fetch_rows(uint64_t (&raw)[8], const uint8_t *fb, bool fb_aligned, const BlockPos &p,
+                                           bool active) {
+  // offsets < the frame size < 2^32, operands < 2^24
+  const uint32_t off = p.poff + (uint32_t)__umul24((uint32_t)p.y0, (uint32_t)p.stride) + (uint32_t)p.x0;
+  const bool fast = fb_aligned && active && (p.x0 + 8 <= p.pw) && (p.y0 + 8 <= p.ph) &&
+                    ((off | (uint32_t)p.stride) & 7) == 0;
+  uint32_t o = fast ? off : 0u;
+  const uint32_t st = fast ? (uint32_t)p.stride : 0u;
   // plain loads: a chunk's row segments straddle 64-B sectors shared with the
   // neighbouring chunk, which L2 keeps for its wave (nontemporal loads read 1.64x)
 #pragma unroll
-  for (int r = 0; r < 8; r++) raw[r] = *(const uint64_t *)(p + r * st);
+  for (int r = 0; r < 8; r++, o += st) raw[r] = *(const uint64_t *)(fb + o);
   return fast;
 }
 
-__device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s) {
+__device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const uint8_t *fb, const BlockPos &p) {
   for (int r = 0; r < 8; r++) {
-    const uint8_t *row = s.plane + (size_t)min(s.y0 + r, s.ph - 1) * s.stride;
+    const uint8_t *row = fb + p.poff + (size_t)min(p.y0 + r, p.ph - 1) * p.stride;
     uint64_t w = 0;
-    for (int b = 0; b < 8; b++) w |= (uint64_t)row[min(s.x0 + b, s.pw - 1)] << (8 * b);
+    for (int b = 0; b < 8; b++) w |= (uint64_t)row[min(p.x0 + b, p.pw - 1)] << (8 * b);
     raw[r] = w;
   }
 }
@@ -508,32 +555,24 @@ __device__ __forceinline__ void fetch_rows_edge(uint64_t (&raw)[8], const Src &s
 // prefetches the next chunk's pixel rows into registers while encoding the current one.
 constexpr int kWavesPerWg = 4;
 
-// Source rectangle of block b (index in the frame's coding order) of `frame`.
-__device__ __forceinline__ Src block_src(const uint8_t *frames, const EncGeom &g, int frame, int b,
-                                         const uint32_t *desc) {
-  const uint8_t *fr = frames + (size_t)frame * g.frame_stride;
-  const int m = (int)__umulhi((uint32_t)b, g.bpm_magic);
-  // (24-bit multiplies: every operand here is below 2^24)
-  const uint32_t d = desc[b - __mul24(m, g.bpm)];
-  const int my = g.mbw == 1 ? m : (int)__umulhi((uint32_t)m, g.mbw_magic), mx = m - __mul24(my, g.mbw);
-  const int plane = (int)(d & 3u), dx = (int)((d >> 3) & 1u) * 8, dy = (int)((d >> 4) & 1u) * 8;
-  Src s;
-  if (plane == 0) {
-    s.plane = fr;
-    s.stride = g.y_stride;
-    s.pw = g.w;
-    s.ph = g.h;
-    s.x0 = __mul24(mx, g.lmw) + dx;
-    s.y0 = my * 16 + dy;
-  } else {
-    s.plane = fr + (plane == 1 ? g.u_off : g.v_off);
-    s.stride = g.c_stride;
-    s.pw = g.cw;
-    s.ph = g.ch;
-    s.x0 = mx * 8 + dx;
-    s.y0 = __mul24(my, g.cmh) + dy;
+// The block-of-MCU descriptor table (BlockDesc) from the descriptor words and the geometry.
+__device__ __forceinline__ void init_block_desc(const EncGeom &g, const uint32_t *tabs, uint4 *s_bd, int tid) {
+  if (tid < 8) {
+    const uint32_t d = tabs[672 + tid];
+    const uint32_t plane = d & 3u;
+    const bool luma = plane == 0;
+    uint4 a, c;
+    a.x = luma ? 0u : (uint32_t)(plane == 1 ? g.u_off : g.v_off);
+    a.y = (uint32_t)(luma ? g.y_stride : g.c_stride);
+    a.z = (uint32_t)(luma ? g.w : g.cw);
+    a.w = (uint32_t)(luma ? g.h : g.ch);
+    c.x = (uint32_t)(luma ? g.lmw : 8);
+    c.y = (uint32_t)(luma ? 16 : g.cmh);
+    c.z = ((d >> 3) & 1u) * 8u;
+    c.w = ((d >> 4) & 1u) * 8u;
+    s_bd[2 * tid] = a;
+    s_bd[2 * tid + 1] = c;
   }
-  return s;
 }
 
 // Task t (one chunk) -> frame, chunk index in its segment, first block of the segment.
@@ -560,15 +599,15 @@ constexpr int kBatchOf = MF ? 8 : 12;
 // lane 56+i holding block chunk*64-8+i of the segment.  Quantised DC = (pixel sum + 32) >> 6
 // exactly.  carry_row: lane loads row (lane & 7) of block (lane >> 3) of those 8 blocks
 // (issued early so the load overlaps a chunk's work); carry_finish reduces them.
-__device__ __forceinline__ uint64_t carry_row(const uint8_t *frames, const EncGeom &g, int frame,
-                                              int bbase, int chunk, int lane, const uint32_t *desc) {
+__device__ __forceinline__ uint64_t carry_row(const uint8_t *fb, const EncGeom &g, int bbase, int chunk, int lane,
+                                              const uint4 *s_bd) {
   if (chunk == 0) return 0;
-  const Src s = block_src(frames, g, frame, bbase + chunk * 64 - 8 + (lane >> 3), desc);
-  const uint8_t *row = s.plane + (size_t)min(s.y0 + (lane & 7), s.ph - 1) * s.stride;
-  if (s.x0 + 8 <= s.pw && (((uintptr_t)(row + s.x0)) & 7) == 0)
-    return *(const uint64_t *)(row + s.x0);
+  const BlockPos p = block_pos(g, bbase + chunk * 64 - 8 + (lane >> 3), s_bd);
+  const uint8_t *row = fb + p.poff + (size_t)min(p.y0 + (lane & 7), p.ph - 1) * p.stride;
+  if (p.x0 + 8 <= p.pw && (((uintptr_t)(row + p.x0)) & 7) == 0)
+    return *(const uint64_t *)(row + p.x0);
   uint64_t w = 0;
-  for (int x = 0; x < 8; x++) w |= (uint64_t)row[min(s.x0 + x, s.pw - 1)] << (8 * x);
+  for (int x = 0; x < 8; x++) w |= (uint64_t)row[min(p.x0 + x, p.pw - 1)] << (8 * x);
   return w;
 }
 
@@ -671,14 +710,17 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
 
 // Row pass of one chunk, lane = block: raw rows (8 little-endian words of 8 pixels) ->
 // the wave's LDS row image s_pk ([word][lane], u16 pairs of value + 32768).
+// The fp32 outputs of columns 0 and 1 (kMb + value) also stay in c01[2 r], c01[2 r + 1]: the
+// column screen's pair 0, which is never skipped, takes them from registers instead of
+// re-reading and unpacking the row image.
 template <bool RC>
 __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, const uint8_t *s_rc,
-                                         uint32_t *s_pk, int lane) {
+                                         uint32_t *s_pk, int lane, float (&c01)[16]) {
   // Row pass (jfdctint pass 1) in fp32, exactly: every value is an integer or a multiple
   // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
   // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
   // (M' = 1.5*2^23 + 32768), which also leaves x + 32768 in the low 16 mantissa bits:
-  // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
+  // its low half goes to the wave's LDS row image as a u16.
   // [RC] swscale tv->pc per pixel from a 512-byte LDS table (clip_u8((p * A21 - B21) >> 21),
   // checked exhaustively in tests/test_oracle.py), OR'ed into the mantissa of M = 1.5*2^23:
   // values then carry the +M bias, which the butterfly's differences cancel and its sums
@@ -730,10 +772,15 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
            __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMb;
     o[7] = __builtin_fmaf(t7, 2260.0f / 512, __builtin_fmaf(t6, -6436.0f / 512,
            __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMb;
+    // the low 16 bits (value + 32768) straight to the u16 halves of the image words: 8
+    // ds_write_b16 instead of 4 v_perm + 4 ds_write_b32 (LDS stores cost no VALU issue)
+    // (LDS pointer, volatile: the compiler would merge the two halves back into perm + b32)
+    volatile __attribute__((address_space(3))) uint16_t *pk16 =
+        (volatile __attribute__((address_space(3))) uint16_t *)s_pk;
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      s_pk[(r * 4 + j) * 64 + lane] =
-          __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
+    for (int j = 0; j < 8; j++) pk16[((r * 4 + (j >> 1)) * 64 + lane) * 2 + (j & 1)] = (uint16_t)__float_as_uint(o[j]);
+    c01[2 * r] = o[0];
+    c01[2 * r + 1] = o[1];
     __builtin_amdgcn_sched_barrier(0);
   }}
 
@@ -745,13 +792,14 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
   // (exact_coef).  Rows 0 and 4 (sums only) are exact, which gives the DC exactly:
   // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
 __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, const uint32_t *s_skip,
-                                              const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb) {
+                                              const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb,
+                                              const float (&c01)[16]) {
 #pragma unroll
   for (int jp = 0; jp < 4; jp++) {
     __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
     uint32_t w[8];
 #pragma unroll
-    for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
+    for (int r = 0; r < 8; r++) w[r] = jp ? s_pk[(r * 4 + jp) * 64 + lane] : 0u;  // pair 0: c01
     // Column skip (pairs 1-3): every AC output of a column quantises to zero when the
     // column's row-pass values are small enough.  Rows 1-7 of pass 2 have coefficient
     // sums 0, so |S_k| <= L1(row k) * R / 2 with R = max - min of the column; row 0 is
@@ -788,7 +836,8 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
       float x[8];
 #pragma unroll
       for (int r = 0; r < 8; r++)
-        x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));
+        x[r] = jp ? __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u))
+                  : c01[2 * r + h];
       // x = M' + value: differences cancel the bias, sums drop it with one -2M'
       const float t0 = (x[0] - 2.0f * kMb) + x[7], t7 = x[0] - x[7];
       const float t1 = (x[1] - 2.0f * kMb) + x[6], t6 = x[1] - x[6];
@@ -1061,6 +1110,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint8_t s_rc[RC ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint4 s_f[MF ? 12 * 64 : 1];  // MFMA A fragments (dct_mfma): [0, 2) pass 1, [4, 12) pass 2
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
+  __shared__ uint4 s_bd[16];                       // their plane fields (BlockDesc)
   __shared__ uint32_t s_skip[SCR ? 12 : 1];        // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
@@ -1081,6 +1131,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   if (tid < 8) {
     s_desc[tid] = tabs[672 + tid];
   }
+  init_block_desc(g, tabs, s_bd, tid);
   if (SCR && tid < 12) s_skip[tid] = tabs[680 + tid];
   if (MF)
     for (int i = tid; i < 12 * 64; i += 64 * kWavesPerWg) s_f[i] = ((const uint4 *)(tabs + kMfTabOff))[i];
@@ -1122,10 +1173,12 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   task_pos(g, t, frame, chunk, bbase);
   int b = chunk * 64 + lane;  // block in the segment
   bool active = b < nblk;
+  // the chunk's frame base (wave-uniform) and whether it is 8-byte aligned
+  auto frame_base = [&](int f) { return frames + (size_t)f * g.frame_stride; };
+  const uint8_t *fb = frame_base(frame);
   uint64_t raw[8];
-  bool fast = fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc), active, frames);
-  int carry = carry_finish(carry_row(frames, g, frame, bbase, chunk, lane, s_desc), chunk, lane, rc, g,
-                           s_desc);
+  bool fast = fetch_rows(raw, fb, ((uintptr_t)fb & 7) == 0, block_pos(g, bbase + b, s_bd), active);
+  int carry = carry_finish(carry_row(fb, g, bbase, chunk, lane, s_bd), chunk, lane, rc, g, s_desc);
 
   while (true) {
     // the next unit is reserved at the top of this unit's last chunk (its rows are prefetched
@@ -1134,13 +1187,14 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     if (t + 1 == tend && lane == 0) nb = (uint32_t)xu.next(work_ctr, nwg);
     const uint32_t dsc = s_desc[block_in_mcu(g, b)];
     const int tab = desc_tab(dsc);
-    if (active && !fast) fetch_rows_edge(raw, block_src(frames, g, frame, bbase + b, s_desc));
+    if (active && !fast) fetch_rows_edge(raw, fb, block_pos(g, bbase + b, s_bd));
     int dc = 0;
     uint64_t mask = 0;
+    float c01[16];
     if (MF)
       mask = dct_mfma<RC>(raw, tab, s_rc, s_f, s_pk, lane, dc);
     else
-      row_pass<RC>(raw, tab, s_rc, s_pk, lane);
+      row_pass<RC>(raw, tab, s_rc, s_pk, lane, c01);
     // prefetch the next chunk while this one is encoded
     const int cur_frame = frame, cur_chunk = chunk, cur_bbase = bbase;
     const bool cur_active = active;
@@ -1154,14 +1208,15 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       task_pos(g, tn, frame, chunk, bbase);
       b = chunk * 64 + lane;
       active = b < nblk;
-      fast = fetch_rows(raw, block_src(frames, g, frame, bbase + b, s_desc), active, frames);
+      fb = frame_base(frame);
+      fast = fetch_rows(raw, fb, ((uintptr_t)fb & 7) == 0, block_pos(g, bbase + b, s_bd), active);
     }
     // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
-    const uint64_t crow = (new_batch && tn >= 0) ? carry_row(frames, g, frame, bbase, chunk, lane, s_desc) : 0;
+    const uint64_t crow = (new_batch && tn >= 0) ? carry_row(fb, g, bbase, chunk, lane, s_bd) : 0;
 
     uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
     if (cur_active) {
-      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
+      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb, c01);
       if (g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
@@ -1192,9 +1247,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       aux_frame = cur_frame;
     }
     if (MODE == kCount) {
-      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kSymCap * 64 + lane};
+      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kRecWords * 64 + lane};
       if (cur_active) emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
-      symn[(size_t)t * 64 + lane] = cs.n;
+      symn[(size_t)t * 64 + lane] = cs.finish();
       if (tn < 0) break;
       if (new_batch) {
         carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
@@ -1244,10 +1299,13 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
 }
 
 // ------------------------------------------------------------ k_emit_syms
-// -huffman optimal, emission pass: every block's symbols as the counting pass recorded
-// them (CountSink), coded with the frame's tables (k_huff_build) and packed as k_encode
-// packs them.  No pixels, no DCT: one wave per chunk, lane = block; the record words are
-// loaded 8 per step (4: 2.5% slower on c1).  Persistent waves (the long-block staging columns are per wave).
+// -huffman optimal, emission pass: every block's symbols as the counting pass recorded them
+// (CountSink's bit stream), coded with the frame's tables (k_huff_build) and packed as
+// k_encode packs them.  No pixels, no DCT: one wave per chunk, lane = block.  A lane decodes
+// its stream from a window of kRecPre words: the chunk's counts and first words are loaded one
+// chunk ahead, and every word the window retires loads the one kRecPre words on (only longer
+// blocks get there).  Persistent waves (the long-block staging columns are per wave).
+constexpr int kRecPre = 4;
 __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
     EncGeom g, const uint32_t *__restrict__ tabs, const uint32_t *__restrict__ ftabs,
     const uint32_t *__restrict__ syms, const uint32_t *__restrict__ symn, uint32_t *__restrict__ scratch,
@@ -1260,24 +1318,25 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
   uint32_t *s_aux = s_aux_all[wave];
   const int nwaves = gridDim.x * kWavesPerWg, gw = blockIdx.x * kWavesPerWg + wave;
   int aux_frame = -1;
-  // the chunk's symbol count and first 8 records are loaded one chunk ahead (the records
-  // past a block's count are never used, and every one of them is inside the record array)
-  uint32_t n_nx = 0, e_nx[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  uint32_t c_nx = 0, e_nx[kRecPre] = {};
   auto head = [&](int tt) {
     int frame, chunk, bbase;
     task_pos(g, tt, frame, chunk, bbase);
     const int b = chunk * 64 + lane;
-    n_nx = b < g.seg_blocks ? symn[(size_t)tt * 64 + lane] : 0u;
-    const uint32_t *rec = syms + (size_t)tt * kSymCap * 64 + lane;
+    c_nx = b < g.seg_blocks ? symn[(size_t)tt * 64 + lane] : 0u;
+    const uint32_t nw = c_nx >> 8;
+    const uint32_t *rec = syms + (size_t)tt * kRecWords * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < 8; i++) e_nx[i] = rec[i * 64];
+    for (int i = 0; i < kRecPre; i++) e_nx[i] = (uint32_t)i < nw ? rec[i * 64] : 0u;
   };
   if (gw < ntasks) head(gw);
   for (int t = gw; t < ntasks; t += nwaves) {
     int frame, chunk, bbase;
     task_pos(g, t, frame, chunk, bbase);
-    const uint32_t n = n_nx;
-    uint32_t e[8] = {e_nx[0], e_nx[1], e_nx[2], e_nx[3], e_nx[4], e_nx[5], e_nx[6], e_nx[7]};
+    const uint32_t n = c_nx & 0xffu, nw = c_nx >> 8;
+    uint32_t e[kRecPre];
+#pragma unroll
+    for (int i = 0; i < kRecPre; i++) e[i] = e_nx[i];
     if (t + nwaves < ntasks) head(t + nwaves);
     if (frame != aux_frame) {  // the frame's code tables into the wave's LDS
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1292,20 +1351,27 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
     q.act = s_aux + tab * 256;
     q.dct = s_aux + 512 + tab * 16;
     q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
-    const uint32_t *rec = syms + (size_t)t * kSymCap * 64 + lane;
-    for (uint32_t j0 = 0; j0 < n; j0 += 8) {
-      if (j0) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) e[i] = j0 + i < n ? rec[(j0 + i) * 64] : 0u;
+    const uint32_t *rec = syms + (size_t)t * kRecWords * 64 + lane;
+    uint32_t p = 0, next = kRecPre;  // bit position in e[0]; the stream word e[kRecPre - 1] loads next
+    for (uint32_t r = 0; r < n; r++) {
+      const uint32_t pk = p ? __builtin_amdgcn_alignbit(e[0], e[1], 32u - p) : e[0];  // 32 bits at p
+      uint32_t len;
+      if (r == 0) {  // DC: category, mantissa
+        const uint32_t cat = pk >> 28;
+        q.dc((int)cat, (pk >> (28u - cat)) & ((1u << cat) - 1u));
+        len = 4 + cat;
+      } else {  // AC: (run, size) byte, mantissa
+        const uint32_t sym = pk >> 24, cat = sym & 15u;
+        q.ac((int)sym, (int)cat, (pk >> (24u - cat)) & ((1u << cat) - 1u));
+        len = 8 + cat;
       }
+      p += len;
+      if (p >= 32) {  // e[0] retired: shift the window, load the word kRecPre on
+        p -= 32;
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        if (j0 + i >= n) break;
-        const uint32_t v = (e[i] >> 16) & 0xffu, mant = e[i] & 0xffffu;
-        if (e[i] >> 31)
-          q.dc((int)v, mant);
-        else
-          q.ac((int)v, (int)(v & 15u), mant);
+        for (int i = 0; i + 1 < kRecPre; i++) e[i] = e[i + 1];
+        e[kRecPre - 1] = next < nw ? rec[next * 64] : 0u;
+        next++;
       }
     }
     if (q.bits > 128) q.flush();
@@ -1575,8 +1641,8 @@ __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk
                                                     uint32_t *__restrict__ work_ctr,
                                                     uint32_t *__restrict__ status) {
   const int f = blockIdx.x;
-  if (f == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;  // k_encode's unit counters
-  if (f == 0 && threadIdx.x == 0) *status = 0;  // output overflow flag, set by k_frame_hdr
+  if (f == 0 && threadIdx.x <= kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;  // k_encode's unit counters, k_stuff's ticket
+  if (f == 0 && threadIdx.x == 0) *status = 0;  // output overflow flag, set by k_stuff
   uint32_t *cb = chunk_bits + (size_t)f * nchunks;
   for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
   __syncthreads();
@@ -1604,7 +1670,7 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
                                                        int nsegs, uint32_t *__restrict__ work_ctr,
                                                        uint32_t *__restrict__ status) {
   const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
+  if (blockIdx.x == 0 && threadIdx.x <= kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *status = 0;
   if (sg >= nsegs) return;
   uint32_t *cb = chunk_bits + (size_t)sg * nchunks;
@@ -1613,13 +1679,13 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
   if (lane == 0) seg_bits[sg] = t;
 }
 
-// Realign/stuff kernels work on *groups* of kChunksPerWave consecutive chunks of an
+// k_stuff works on *groups* of kChunksPerWave consecutive chunks of an
 // entropy-coded segment (the frame unless RST mode), one wave per group, lanes = the group's
 // words flattened across its chunks.  A word belongs to the chunk holding its first bit, so
 // chunk c owns words [ceil(O_c / 32), ceil(O_{c+1} / 32)) and a group owns one contiguous
 // word range.  Everything per group (offsets, lengths) lives in lane registers, so a word
-// costs only its slot loads, and a round issues all of them before any is used: the kernels
-// are load-latency bound (one wave per ~200 words), not bandwidth bound.
+// costs only its slot loads, and a round issues all of them before any is used: the pass
+// is load-latency bound (one wave per ~200 words), not bandwidth bound.
 constexpr int kChunksPerWave = 8;
 constexpr int kWordsPerLane = 4;  // words per lane per round
 
@@ -1713,207 +1779,200 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
-__global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
-                                                  const uint32_t *__restrict__ chunk_bits,
-                                                  const uint32_t *__restrict__ chunk_off,
-                                                  const uint32_t *__restrict__ frame_bits,
-                                                  uint32_t *__restrict__ group_ff, int nchunks,
-                                                  int ngroups_per_frame, int ngroups) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (gi >= ngroups) return;
-  const GroupWords g =
-      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
-  int cnt = 0;
-  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
-    WordLoad ld[kWordsPerLane];
+// ----------------------------------------------------------------- k_stuff
+// The whole stuffing tail in one pass: replaces k_count_ff -> k_scan_ff (-> k_scan_ff_seg,
+// k_seg_sizes) -> k_frame_hdr -> k_write, which read every slot twice and cost four more
+// launches beside the next submit's k_encode.  One wave per group of kChunksPerWave chunks,
+// groups in submit order (frame, entropy-coded segment, group), each taking a ticket so every
+// smaller ticket is already held by a running wave:
+//   1. the group's owned words (realigned to the segment's bit offsets from k_scan_bits, the
+//      last byte padded with 1s) and their 0xFF count;
+//   2. its aggregate A = owned bytes + 0xFFs (+ the frame header for the frame's first group,
+//      + the 2-byte RSTn / EOI trailer for the segment's last group), published at once;
+//   3. decoupled look-back over the predecessors' published words: the exclusive prefix P is
+//      the sum of aggregates back to the nearest published inclusive prefix, then P + A is
+//      published as this group's inclusive prefix;
+//   4. header (first group of a frame), stuffed bytes (ff_mjpeg_escape_FF) and trailer
+//      (mjpegenc.c ff_mjpeg_encode_stuffing RST0 + (mb_y & 7); EOI) written at P; the frame's
+//      last group stores the frame's end offset (frame_offsets[f + 1]).
+// A group whose bytes would pass out_cap writes nothing and sets status bit 0; the offsets are
+// complete either way, so the host regrows the output to frame_offsets[n] and runs the pass
+// again.  The look-back words carry the launch's epoch, so none is reset between launches.
+// Every wave publishes its aggregate before it waits on anything: no wave waits on a wave
+// that waits on it, whatever the placement.
+constexpr int kLbValueBits = 42;
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint32_t flag, uint64_t v) {
+  return ((uint64_t)epoch << (kLbValueBits + 2)) | ((uint64_t)flag << kLbValueBits) | v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
-    uint32_t v[kWordsPerLane];
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) {
-      const uint32_t k = kb + 64 * i + lane;
-      if (k < g.k1) cnt += ff_in_word(v[i], 4 * k, g.total_bytes);
-    }
+  for (int d = 32; d > 0; d >>= 1) v += (uint64_t)__shfl_xor((long long)v, d, 64);
+  return v;
+}
+
+// Frame header bytes [0, hl) at fo: the context's header, or with -huffman optimal its bytes
+// before and after the DHT around the frame's own DHT (jpeg_table_header: one DHT, tables DC0,
+// DC1, AC0, AC1).
+__device__ __forceinline__ void write_frame_header(uint8_t *fo, int f, int lane, const uint8_t *hdr, int hdr_len,
+                                                   const uint32_t *dht_nval, int dht_pos, int dht_end,
+                                                   const uint8_t *dht) {
+  if (!dht_nval) {
+    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
+    return;
   }
-  cnt = wave_sum(cnt);
-  if (lane == 0) group_ff[gi] = (uint32_t)cnt;
+  const uint32_t *nv = dht_nval + 4 * (size_t)f;
+  const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
+  for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
+  uint8_t *o = fo + dht_pos;
+  if (lane == 0) {
+    o[0] = 0xff;
+    o[1] = 0xc4;
+    o[2] = (uint8_t)(len >> 8);
+    o[3] = (uint8_t)len;
+  }
+  o += 4;
+  for (int t = 0; t < 4; t++) {
+    const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
+    const int n = 16 + (int)nv[t];
+    if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
+    for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
+    o += 1 + n;
+  }
+  const int tail = hdr_len - dht_end;
+  for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
 }
 
-// Per frame: exclusive scan of the chunk groups' 0xFF counts -> stuffed frame size.
-// -huffman optimal (dht_nval != null): the header length is per frame, hdr_base plus the
-// frame's table values, stored to hdr_lens for k_frame_hdr / k_write.
-__global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ group_ff,
-                                                  uint32_t *__restrict__ ff_off,
-                                                  const uint32_t *__restrict__ frame_bits,
-                                                  uint64_t *__restrict__ frame_size, int ngroups_per_frame,
-                                                  int hdr_len, const uint32_t *__restrict__ dht_nval,
-                                                  int hdr_base, uint32_t *__restrict__ hdr_lens) {
-  const int f = blockIdx.x;
-  const size_t g0 = (size_t)f * ngroups_per_frame;
-  const uint32_t t = block_excl_scan(group_ff + g0, ff_off + g0, ngroups_per_frame);
-  if (threadIdx.x == 0) {
-    uint32_t hl = (uint32_t)hdr_len;
-    if (dht_nval) {
-      hl = (uint32_t)hdr_base + dht_nval[4 * f] + dht_nval[4 * f + 1] + dht_nval[4 * f + 2] +
-           dht_nval[4 * f + 3];
-      hdr_lens[f] = hl;
-    }
-    frame_size[f] = (uint64_t)hl + ((frame_bits[f] + 7) >> 3) + t + 2;
+// One round of the group's words: lane i holds words kb + 64 j + lane (j < kWordsPerLane).
+struct StuffRound {
+  uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
+};
+
+__device__ __forceinline__ void stuff_round(const GroupWords &g, uint32_t kb, int lane, StuffRound &r) {
+  WordLoad ld[kWordsPerLane];
+#pragma unroll
+  for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
+#pragma unroll
+  for (int i = 0; i < kWordsPerLane; i++) {
+    const uint32_t k = kb + 64 * i + lane;
+    r.v[i] = word_value(g, ld[i], min(k, g.k1 - 1));
+    r.cnt[i] = k < g.k1 ? (uint32_t)ff_in_word(r.v[i], 4 * k, g.total_bytes) : 0u;
   }
 }
 
-// RST mode, per segment (wave): scan of its groups' 0xFF counts -> stuffed segment size
-// including the 2-byte trailer (RSTn or, for the frame's last segment, EOI).
-__global__ __launch_bounds__(256) void k_scan_ff_seg(const uint32_t *__restrict__ group_ff,
-                                                     uint32_t *__restrict__ ff_off,
-                                                     const uint32_t *__restrict__ seg_bits,
-                                                     uint64_t *__restrict__ seg_size, int ngroups_per_seg,
-                                                     int nsegs) {
-  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (sg >= nsegs) return;
-  const size_t g0 = (size_t)sg * ngroups_per_seg;
-  const uint32_t t = wave_excl_scan_arr(group_ff + g0, ff_off + g0, ngroups_per_seg, lane);
-  if (lane == 0) seg_size[sg] = (uint64_t)((seg_bits[sg] + 7) >> 3) + t + 2;
-}
-
-// RST mode (one entropy-coded segment per MCU row): per frame, the segments' offsets after
-// the header (exclusive scan of their stuffed sizes, each including its 2-byte trailer:
-// RSTn, or EOI for the last) and the frame size = header + all segments.
-__global__ __launch_bounds__(64) void k_seg_sizes(const uint64_t *__restrict__ seg_size, int nseg,
-                                                  int hdr_len, uint32_t *__restrict__ seg_off,
-                                                  uint64_t *__restrict__ frame_size) {
-  const int f = blockIdx.x, lane = threadIdx.x;
-  uint32_t carry = 0;
-  for (int s0 = 0; s0 < nseg; s0 += 64) {
-    const int s = s0 + lane;
-    const uint32_t v = s < nseg ? (uint32_t)seg_size[(size_t)f * nseg + s] : 0u;
-    const uint32_t incl = wave_incl_scan(v, lane);
-    if (s < nseg) seg_off[(size_t)f * nseg + s] = carry + incl - v;
+// Stuffed bytes of one round at base (+ carry: 0xFFs of the group's earlier rounds).
+__device__ __forceinline__ void stuff_write(const GroupWords &g, uint32_t kb, int lane, const StuffRound &r,
+                                            uint8_t *base, uint32_t &carry) {
+#pragma unroll
+  for (int i = 0; i < kWordsPerLane; i++) {
+    const uint32_t k = kb + 64 * i + lane;
+    const uint32_t incl = wave_incl_scan(r.cnt[i], lane);
+    if (k < g.k1) {
+      uint8_t *p = base + 4 * (k - g.k0) + carry + incl - r.cnt[i];
+#pragma unroll
+      for (int bb = 0; bb < 4; bb++) {
+        if (4 * k + bb < g.total_bytes) {
+          const uint8_t byte = (uint8_t)(r.v[i] >> (24 - 8 * bb));
+          *p++ = byte;
+          if (byte == 0xff) *p++ = 0;
+        }
+      }
+    }
     carry += lane63(incl);
   }
-  if (lane == 0) frame_size[f] = (uint64_t)hdr_len + carry;
 }
 
-// One wave per frame: packed output offset (sum of the preceding frame sizes), capacity
-// check, header (SOI .. SOS) and EOI of the frame; in RST mode (seg_off != null) also the
-// RST0..7 marker closing every segment but the last (mjpegenc.c ff_mjpeg_encode_stuffing:
-// RST0 + (mb_y & 7) after MCU row mb_y).  -huffman optimal (hdr_lens != null):
-// the default header's bytes before and after its DHT around the frame's own DHT
-// (jpeg_table_header: one DHT, tables DC0, DC1, AC0, AC1).
-__global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ frame_size,
-                                                  const uint8_t *__restrict__ hdr, int hdr_len,
-                                                  uint8_t *__restrict__ out, uint64_t out_cap,
-                                                  uint64_t *__restrict__ frame_offsets,
-                                                  uint32_t *__restrict__ status,
-                                                  const uint32_t *__restrict__ hdr_lens, int dht_pos,
-                                                  int dht_end, const uint8_t *__restrict__ dht,
-                                                  const uint32_t *__restrict__ dht_nval,
-                                                  const uint32_t *__restrict__ seg_off,
-                                                  const uint64_t *__restrict__ seg_size, int nseg) {
-  const int f = blockIdx.x, lane = threadIdx.x;
-  uint64_t s = 0;
-  for (int i = lane; i < f; i += 64) s += frame_size[i];
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
-  const uint64_t fsize = frame_size[f];
-  if (lane == 0) {
-    frame_offsets[f] = s;
-    if (f == (int)gridDim.x - 1) frame_offsets[f + 1] = s + fsize;
+__global__ __launch_bounds__(256) void k_stuff(
+    const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
+    const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ seg_bits, int nchunks, int gps,
+    int ngroups, int nseg, const uint8_t *__restrict__ hdr, int hdr_len,
+    const uint32_t *__restrict__ dht_nval, int dht_pos, int dht_end, const uint8_t *__restrict__ dht,
+    uint8_t *__restrict__ out, uint64_t out_cap, uint64_t *__restrict__ frame_offsets,
+    uint32_t *__restrict__ status, uint64_t *__restrict__ lb, uint32_t epoch, uint32_t *__restrict__ ticket) {
+  const int lane = threadIdx.x & 63;
+  int t = 0;
+  if (lane == 0) t = (int)atomicAdd(ticket, 1u);
+  const int gi = __builtin_amdgcn_readfirstlane(t);
+  if (gi >= ngroups) return;
+  const GroupWords g = group_words(scratch, chunk_bits, chunk_off, seg_bits, nchunks, gps, gi, lane);
+  const int fr = g.f / nseg, sif = g.f - fr * nseg;  // frame, segment in the frame
+  const bool first = sif == 0 && g.c0 == 0;
+  const bool last = g.c0 + kChunksPerWave >= nchunks;  // the segment's last group
+  uint32_t hl = (uint32_t)hdr_len;
+  if (dht_nval) {  // -huffman optimal: the default header's 348 table values -> the frame's
+    const uint32_t *nv = dht_nval + 4 * (size_t)fr;
+    hl = (uint32_t)hdr_len - 348u + nv[0] + nv[1] + nv[2] + nv[3];
   }
-  if (s + fsize > out_cap) {
+  // 1. owned words and their 0xFF count (one round in registers; longer groups re-load)
+  const uint32_t nwords = g.k1 - g.k0;
+  const bool one_round = nwords <= 64u * kWordsPerLane;
+  StuffRound r0;
+  uint32_t ff = 0;
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
+    StuffRound r;
+    stuff_round(g, kb, lane, r);
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) ff += r.cnt[i];
+    if (kb == g.k0) r0 = r;
+  }
+  ff = (uint32_t)wave_sum((int)ff);
+  const uint32_t owned = min(4 * g.k1, g.total_bytes) - min(4 * g.k0, g.total_bytes);
+  const uint64_t agg = (uint64_t)owned + ff + (first ? hl : 0u) + (last ? 2u : 0u);
+  // 2. publish the aggregate (group 0: its inclusive prefix)
+  if (lane == 0)
+    __hip_atomic_store(lb + gi, lb_word(epoch, gi == 0 ? 2u : 1u, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // 3. look back
+  uint64_t excl = 0;
+  constexpr uint64_t kVal = (1ull << kLbValueBits) - 1;
+  for (int end = gi; end > 0; end -= 64) {
+    const int j = end - 1 - lane;  // lane 0: the nearest predecessor
+    uint64_t w;
+    uint64_t incl_mask;
+    while (true) {
+      w = j >= 0 ? __hip_atomic_load(lb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : lb_word(epoch, 2u, 0);
+      const bool ready = (uint32_t)(w >> (kLbValueBits + 2)) == epoch && ((w >> kLbValueBits) & 3u) != 0;
+      incl_mask = __ballot(ready && ((w >> kLbValueBits) & 3u) == 2u);
+      const uint64_t waiting = __ballot(!ready);
+      // usable when every predecessor up to the nearest inclusive prefix (or the whole window)
+      // has published
+      const uint64_t need = incl_mask ? ((incl_mask & (~incl_mask + 1)) << 1) - 1 : ~0ull;
+      if (!(waiting & need)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const int stop = incl_mask ? (int)__builtin_ctzll(incl_mask) : 63;
+    excl += wave_sum64(lane <= stop ? (w & kVal) : 0ull);
+    if (incl_mask) break;
+  }
+  if (gi > 0 && lane == 0)
+    __hip_atomic_store(lb + gi, lb_word(epoch, 2u, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    if (gi == 0) frame_offsets[0] = 0;
+    if (last && sif == nseg - 1) frame_offsets[fr + 1] = excl + agg;
+  }
+  // 4. write
+  if (excl + agg > out_cap) {
     if (lane == 0) atomicOr(status, 1u);
     return;
   }
-  uint8_t *fo = out + s;
-  if (!hdr_lens) {
-    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
-  } else {
-    const uint32_t *nv = dht_nval + 4 * (size_t)f;
-    const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
-    for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
-    uint8_t *o = fo + dht_pos;
-    if (lane == 0) {
-      o[0] = 0xff;
-      o[1] = 0xc4;
-      o[2] = (uint8_t)(len >> 8);
-      o[3] = (uint8_t)len;
-    }
-    o += 4;
-    for (int t = 0; t < 4; t++) {
-      const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
-      const int n = 16 + (int)nv[t];
-      if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
-      for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
-      o += 1 + n;
-    }
-    const int tail = hdr_len - dht_end;
-    for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
+  uint8_t *o = out + excl;
+  if (first) {
+    write_frame_header(o, fr, lane, hdr, hdr_len, dht_nval, dht_pos, dht_end, dht);
+    o += hl;
   }
-  if (lane == 0) {
-    fo[fsize - 2] = 0xff;
-    fo[fsize - 1] = 0xd9;
-  }
-  if (seg_off)
-    for (int sg = lane; sg < nseg - 1; sg += 64) {
-      const size_t i = (size_t)f * nseg + sg;
-      uint8_t *m = fo + hdr_len + seg_off[i] + seg_size[i] - 2;
-      m[0] = 0xff;
-      m[1] = (uint8_t)(0xd0 + (sg & 7));
-    }
-}
-
-// Wave per chunk group, lanes = words: the group's owned bytes with a 0x00 after every
-// 0xFF (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs before it in the
-// frame (group prefix from k_scan_ff, in-group prefix by a wave scan).
-__global__ __launch_bounds__(256) void k_write(
-    const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
-    const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
-    const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
-    const uint64_t *__restrict__ frame_offsets, int hdr_len, const uint32_t *__restrict__ hdr_lens,
-    int nchunks, int ngroups_per_frame, int ngroups, uint8_t *__restrict__ out, uint64_t out_cap,
-    const uint32_t *__restrict__ seg_off, int nseg) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (gi >= ngroups) return;
-  // g.f is the entropy-coded segment (the frame itself unless RST mode)
-  const GroupWords g =
-      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
-  const int fr = g.f / nseg;
-  const uint64_t foff = frame_offsets[fr];
-  if (foff + frame_size[fr] > out_cap) return;  // k_frame_hdr flagged the overflow
-  const uint32_t hl = hdr_lens ? hdr_lens[fr] : (uint32_t)hdr_len;
-  uint8_t *base = out + foff + hl + (seg_off ? seg_off[g.f] : 0u) + 4 * (size_t)g.k0 + ff_off[gi];
   uint32_t carry = 0;
-  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
-    WordLoad ld[kWordsPerLane];
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
-    uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) {
-      const uint32_t k = kb + 64 * i + lane;
-      cnt[i] = k < g.k1 ? (uint32_t)ff_in_word(v[i], 4 * k, g.total_bytes) : 0u;
+  if (one_round) {
+    if (nwords) stuff_write(g, g.k0, lane, r0, o, carry);
+  } else {
+    for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
+      StuffRound r;
+      stuff_round(g, kb, lane, r);
+      stuff_write(g, kb, lane, r, o, carry);
     }
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) {
-      const uint32_t k = kb + 64 * i + lane;
-      const uint32_t incl = wave_incl_scan(cnt[i], lane);
-      if (k < g.k1) {
-        uint8_t *p = base + 4 * (k - g.k0) + carry + incl - cnt[i];
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-          if (4 * k + bb < g.total_bytes) {
-            const uint8_t byte = (uint8_t)(v[i] >> (24 - 8 * bb));
-            *p++ = byte;
-            if (byte == 0xff) *p++ = 0;
-          }
-        }
-      }
-      carry += lane63(incl);
-    }
+  }
+  if (last && lane == 0) {
+    uint8_t *m = out + excl + agg - 2;
+    m[0] = 0xff;
+    m[1] = sif == nseg - 1 ? 0xd9 : (uint8_t)(0xd0 + (sif & 7));
   }
 }
 

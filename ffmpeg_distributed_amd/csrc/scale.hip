@@ -43,7 +43,7 @@ __host__ __device__ constexpr int scale_loads_per_wave(int th) { return th >= 64
 __host__ __device__ constexpr int scale_waves(int th) { return th == 128 ? 8 : 4; }
 constexpr int kScaleAliasWords = 36;  // TH 64: LDS row stride (dwords), the widest fast window
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+typedef u32x4 u32x4_a1 __attribute__((aligned(1)));  // window pieces start at any byte
 
 struct ScaleGeom {
   int sw, sh, dw, dh;            // plane sizes
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
       const int r = ALIAS ? 2 * ppw * wave + kScaleLoadRows * i + rr : kScaleLoadRows * (LPW * wave + i) + rr;
       const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
       if (col + 16 <= g.sw) {
-        v[i] = *(const u32x4_a4 *)(rp + col);
+        v[i] = *(const u32x4_a1 *)(rp + col);
       } else {  // the piece crosses the row end: dwords loaded in-row and shifted down (bytes
                 // >= sw meet no tap)
         uint32_t w[4];

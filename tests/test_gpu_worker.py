@@ -197,10 +197,11 @@ def test_resident_client_segments_match_oracle(tmp_path):
         for i, (w, h, q, n) in enumerate(cases):
             frames = [make_testsrc(w, h, 13 * i + k) for k in range(n)]
             (tmp_path / f"in{i}.mkv").write_bytes(_raw_mkv(frames, w, h))
+            seen = []
             with open(tmp_path / f"in{i}.mkv", "rb") as fi, open(tmp_path / f"out{i}.mkv", "wb") as fo:
-                p = D.FFMPEGProc(argv, stdin=fi, stdout=fo)
+                p = D.FFMPEGProc(argv, stdin=fi, stdout=fo, update_callback=lambda *a: seen.append(a))
                 assert p.run() == 0, p.stderr
-            assert p.duration is not None
+            assert seen and seen[-1][0] == n  # the final progress line counts every frame
             r = container.MkvReader(io.BytesIO((tmp_path / f"out{i}.mkv").read_bytes()))
             want = [oracle.encode_frame(*split_i420(f, w, h), full_range=False, qscale=q, sar=(1, 1)) for f in frames]
             assert [d for _, d in r.frames(1)] == want, f"segment {i}"

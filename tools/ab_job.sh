@@ -12,7 +12,7 @@ for w in "$@"; do
   for i in 1 2; do
     for v in old new; do
       if [ $v = old ]; then export MJG_LIBRARY=$OLD; else unset MJG_LIBRARY; fi
-      timeout -k 10 200 python bench.py --no-cpu-baseline --workload $w > $O/$w.$v$i.json 2>>$O/err.log || exit $?
+      timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --workload $w > $O/$w.$v$i.json 2>>$O/err.log || exit $?
       python -c "import json,sys; d=json.load(open('$O/$w.$v$i.json')); print('$w $v$i', d['value'], {k:v for k,v in d['kernel_ms_per_step'].items() if v})"
     done
   done
