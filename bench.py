@@ -234,7 +234,9 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
             r = leg(per_process(True), segments)
             r["argv"] = "mjg_client --device N -- <remote_args> (resident encoder per GPU)"
             out["per_segment_process"] = r
-            subprocess.run([D.CLIENT, "--device", str(device), "--shutdown"], timeout=60)
+            from ffmpeg_distributed_amd import resident
+            if not resident.shutdown(D.CLIENT, device):
+                r["warning"] = "resident encoder still running after its shutdown"
         srv = D.GpuServer(host)
         try:
             r = leg(lambda dst: srv.run_task(D.Task(seg, dst, args)), segments)

@@ -13,8 +13,7 @@
 // the same end of stream and exit code as from ffmpeg.
 //
 // If no resident encoder listens (first segment, or it exited after its idle timeout), the
-// client starts one as a new session, with no descriptor of the segment inherited, and then
-// connects.  This process never touches the GPU, so starting the encoder with fork + exec is
+// client starts one, with no descriptor of the segment inherited, and then connects.  This process never touches the GPU, so starting the encoder with fork + exec is
 // safe.  The socket lives in the abstract namespace; its name carries the user id, the device,
 // the visible-device environment, and the inode and mtime of libmjgpu.so, so a rebuilt library
 // or another device mapping gets a new encoder.  The encoder accepts only peers with its uid.
@@ -105,9 +104,11 @@ static int try_connect(const char *name) {
   return fd;
 }
 
-// Start the resident encoder: a new session, cwd = the package's parent (python -m finds the
-// package there), stdin /dev/null, stdout/stderr to its log (never the segment's pipes: the
-// dispatcher waits for EOF on this process's stderr), no other descriptor inherited.
+// Start the resident encoder: cwd = the package's parent (python -m finds the package there),
+// stdin /dev/null, stdout/stderr to its log (never the segment's pipes: the dispatcher waits for
+// EOF on this process's stderr), no other descriptor inherited.  It stays in the caller's
+// process group (no setsid): whoever stops the dispatcher's job by its group stops the encoder
+// too, and otherwise it ends after its idle timeout.
 static pid_t spawn(const char *python, const char *pkg, const char *dev, const char *name, const char *idle) {
   char root[4096], logp[256];
   snprintf(root, sizeof root, "%s", pkg);
@@ -117,7 +118,6 @@ static pid_t spawn(const char *python, const char *pkg, const char *dev, const c
   snprintf(logp, sizeof logp, "/tmp/%s.log", name);
   const pid_t pid = fork();
   if (pid != 0) return pid;
-  setsid();
   const int nul = open("/dev/null", O_RDONLY);
   int log = open(logp, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0600);
   if (log < 0) log = open("/dev/null", O_WRONLY);

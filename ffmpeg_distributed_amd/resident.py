@@ -10,7 +10,7 @@ contract: segment on stdin, Matroska on stdout, ffmpeg-style progress on stderr,
 
     python -m ffmpeg_distributed_amd.resident --device N --socket NAME [--idle SECONDS]
 
-mjg_client starts it (a new session, stdio on its log file) when no encoder listens on
+mjg_client starts it (stdio on its log file, in the caller's process group) when no encoder listens on
 NAME, an abstract-namespace socket.  Each connection is one request (wire format in
 mjg_client.c): an encode request carries the remote_args, the client's MJG_* environment
 and its three descriptors; `worker.run` encodes the segment from them on a thread of its
@@ -209,6 +209,26 @@ class Resident:
             for c in caches:
                 worker.release(c)
         return 0
+
+
+def shutdown(client: str, device: int, timeout: float = 30.0) -> bool:
+    """Ask the resident encoder of `device` to exit (`mjg_client --shutdown`) and wait until its
+    socket refuses connections; True when none runs any more."""
+    import subprocess
+    subprocess.run([client, "--device", str(device), "--shutdown"], timeout=timeout)
+    name = subprocess.run([client, "--device", str(device), "--socket-name"], capture_output=True,
+                          text=True, timeout=timeout).stdout.strip()
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout:
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        try:
+            s.connect("\0" + name)
+        except OSError:
+            return True
+        finally:
+            s.close()
+        time.sleep(0.1)
+    return False
 
 
 def listen(name: str) -> socket.socket:

@@ -213,3 +213,23 @@ def test_resident_client_segments_match_oracle(tmp_path):
                     assert p.run() == 1 and "ends inside a frame" in p.stderr
     finally:
         subprocess.run([client, "--device", "0", "--shutdown"], timeout=60)
+        _wait_resident_gone(client, "0")
+
+
+def _wait_resident_gone(client, dev, timeout=30.0):
+    """The resident encoder has exited (its socket refuses connections)."""
+    import socket
+    import subprocess
+    import time
+    name = subprocess.run([client, "--device", dev, "--socket-name"], capture_output=True, text=True).stdout.strip()
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout:
+        s = socket.socket(socket.AF_UNIX)
+        try:
+            s.connect("\0" + name)
+        except OSError:
+            return
+        finally:
+            s.close()
+        time.sleep(0.2)
+    raise AssertionError("resident encoder still running after its shutdown")
