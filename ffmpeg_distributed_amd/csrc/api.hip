@@ -189,7 +189,7 @@ struct Slot {
   uint64_t *h_sizes = nullptr;   // page-locked: frame offsets [0, n] of the submit (k_stuff)
   uint32_t *h_status = nullptr;
   std::vector<uint64_t> sizes;   // frame sizes, from h_sizes at sync
-  uint64_t *d_lb = nullptr;      // k_stuff's look-back words, one per chunk group
+  uint64_t *d_lb = nullptr;      // k_stuff's look-back words, one per tile of chunk groups
   uint32_t epoch = 0;            // k_stuff launch tag of this slot (1 .. kMaxEpoch)
   hipEvent_t done = nullptr, enc_done = nullptr;
   hipEvent_t ev[MJG_NUM_KERNELS][2] = {};
@@ -409,7 +409,7 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   if (c->optimal &&
       ((rc = dmalloc(&S.d_hist, B * kFrameTabWords)) || (rc = dmalloc(&S.d_ftabs, B * kFrameTabWords)) ||
        (rc = dmalloc(&S.d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&S.d_dht_nval, B * 4)) ||
-       (rc = dmalloc(&S.d_syms, B * NC * (size_t)kRecWords * 64)) ||
+       (rc = dmalloc(&S.d_syms, B * NC * (size_t)kSymCap * 64)) ||
        (rc = dmalloc(&S.d_symn, B * NC * 64))))
     return rc;
   if (g.debug_coefs && (rc = dmalloc(&S.d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
@@ -805,7 +805,7 @@ int launch_write(mjg_ctx *c, Slot &S, int n, bool rerun) {
   S.epoch = S.epoch % kMaxEpoch + 1;
   if (S.epoch == 1) HIP_TRY(hipMemsetAsync(S.d_lb, 0, (size_t)ngroups * sizeof(uint64_t), c->tail));
   tmark(c, S, MJG_K_WRITE, 0);
-  k_stuff<<<(ngroups + 3) / 4, 256, 0, c->tail>>>(
+  k_stuff<<<(ngroups + kStuffTile - 1) / kStuffTile, 64 * kStuffWaves, 0, c->tail>>>(
       S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, g.nchunks, gps, ngroups, g.nseg, c->d_hdr,
       (int)c->hdr.size(), c->optimal ? S.d_dht_nval : nullptr, (int)c->dht_pos, (int)c->dht_end, S.d_dht, S.d_out,
       (uint64_t)S.out_cap, S.d_frame_offsets, S.d_status, S.d_lb, S.epoch, S.d_work + kXcds * kCtrStride);

@@ -412,11 +412,10 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
         for (int r = 0; r < 8; r++) raw[r] = active ? *(const uint64_t *)(bp + r * pitch) : 0ull;
       }
       __syncthreads();  // every wave holds its rows: the region becomes the row images
-      float c01[16];
-      row_pass<false>(raw, tab, nullptr, s_pk, lane, c01);
+      row_pass<false>(raw, tab, nullptr, s_pk, lane);
       int dc = 0;
       uint32_t ca = 0, cb = 0;
-      if (active) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb, c01);
+      if (active) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
       const uint64_t mask = screen_mask(ca, cb, s_scat);
       const int par = grp & 1;
       if (lane >= 56) s_dcx[par][wave][lane - 56] = dc;
@@ -426,10 +425,9 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
       const int diff = dc - dc_predictor(dc, carry, desc_delta(dsc), chunk == 0, lane);
       const size_t t = (size_t)frame * g.nchunks + chunk;
       if (MODE == kCount) {
-        CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + t * kRecWords * 64 + lane};
+        CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + t * kSymCap * 64 + lane};
         if (active) emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
-        const uint32_t cnt = cs.finish();
-        if (chunk < g.nchunks) symn[t * 64 + lane] = cnt;
+        if (chunk < g.nchunks) symn[t * 64 + lane] = cs.n;
       } else {
         ShiftSink q;
         q.act = s_ac + tab * 256;

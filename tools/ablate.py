@@ -11,10 +11,10 @@ build are wrong by construction; only kernel times (and SQ counters) are compare
   noexact  : exact_coef returns a constant (the candidate loop and coding kept)
   noscreen : column screen skipped (DC from the row image, no candidates): loads + row pass +
              DC/EOB coding + pack
+  stuff_w4, stuff_w8, stuff_t32: k_stuff with 4 / 8 waves per workgroup, or 32-group tiles
+             (same bytes; for the tail's shape A/B)
   nodct    : row pass and column screen skipped (raw rows copied into the LDS image): loads +
              LDS image + DC/EOB coding + pack
-  nod16, noreg0: not ablations but the round-3 k_encode changes reverted one at a time (the
-             row image stored as packed words, pair 0 read back from LDS): same bytes
 
 usage: tools/ablate.py NAME...      (writes tools/_v<NAME>src/ and builds the .so)
        tools/ablate.py --variants NAME...   (prints the VARIANTS string for variants.py)
@@ -31,28 +31,17 @@ EMIT = ("      emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);\n"
         "      if (q.bits > 128) q.flush();\n")
 WIDE = "const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);"
 EXACT = "  const int ro = n >> 3, c = n & 7;\n  const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;\n  const uint4 mp"
-SCREEN = "      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb, c01);"
-ROWPASS = "      row_pass<RC>(raw, tab, s_rc, s_pk, lane, c01);"
+SCREEN = "      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);"
+ROWPASS = "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);"
 
-# the row pass's output stores (r03: ds_write_b16 per output) and pair 0 of the column screen
-# (r03: from the row pass's registers), each reverted on its own for an A/B
-D16 = ("    // (LDS pointer, volatile: the compiler would merge the two halves back into perm + b32)\n"
-       "    volatile __attribute__((address_space(3))) uint16_t *pk16 =\n"
-       "        (volatile __attribute__((address_space(3))) uint16_t *)s_pk;\n"
-       "#pragma unroll\n"
-       "    for (int j = 0; j < 8; j++) pk16[((r * 4 + (j >> 1)) * 64 + lane) * 2 + (j & 1)] = (uint16_t)__float_as_uint(o[j]);\n")
-PACK = ("#pragma unroll\n"
-        "    for (int j = 0; j < 4; j++)\n"
-        "      s_pk[(r * 4 + j) * 64 + lane] =\n"
-        "          __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);\n")
-REG0_W = "w[r] = jp ? s_pk[(r * 4 + jp) * 64 + lane] : 0u;"
-REG0_X = ("        x[r] = jp ? __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u))\n"
-          "                  : c01[2 * r + h];")
+TILE = "constexpr int kStuffTile = 64;    // groups per workgroup"
+WAVES = "constexpr int kStuffWaves = 16;  // waves per workgroup (kStuffTile / kStuffWaves groups each)"
 
 SUBS = {
-    "nod16": [(D16, PACK)],
-    "noreg0": [(REG0_W, "w[r] = s_pk[(r * 4 + jp) * 64 + lane];"),
-               (REG0_X, "        x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));")],
+    # k_stuff shape (not ablations: same bytes)
+    "stuff_w4": [(WAVES, WAVES.replace("16", "4", 1))],
+    "stuff_w8": [(WAVES, WAVES.replace("16", "8", 1))],
+    "stuff_t32": [(TILE, TILE.replace("64", "32", 1))],
     "noemit": [(EMIT, "      q.emit(((uint32_t)__popcll(mask) << 8) ^ ((uint32_t)diff & 255u), 16);\n"),
                (WIDE, "const uint64_t wide = 0;")],
     "noexact": [(EXACT, "  if (n >= 0) return 1 + (n & 1);\n" + EXACT)],

@@ -36,4 +36,8 @@ done
 unset MJG_LIBRARY
 timeout -k 10 300 python bench.py --cpu-seconds 2 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], json.dumps(d['kernel_ms_per_step'])); print(json.dumps(d['e2e']))"
+
+# disk under the e2e leg's temporary files: filesystem and O_DIRECT read rate of a 1.5 GB file
+{ df -T /tmp; dd if=/dev/zero of=/tmp/mjg_dd bs=16M count=96 oflag=direct 2>&1 | tail -1; dd if=/tmp/mjg_dd of=/dev/null bs=16M iflag=direct 2>&1 | tail -1; dd if=/tmp/mjg_dd of=/dev/null bs=16M 2>&1 | tail -1; rm -f /tmp/mjg_dd; } > $O/disk.txt 2>&1
+cat $O/disk.txt
 echo done
