@@ -176,21 +176,20 @@ struct Slot {
   int n = 0;
   uint64_t total = 0;
   uint32_t *d_scratch = nullptr;
-  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr;
+  uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
   uint32_t *d_frame_bits = nullptr, *d_status = nullptr;
   uint32_t *d_work = nullptr;  // k_encode's batch counter (zero; reset by the slot's scan kernel)
-  uint64_t *d_frame_offsets = nullptr;  // packed output: frame f at [offsets[f], offsets[f + 1])
+  uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
+  uint64_t *d_seg_size = nullptr;  // RST mode: stuffed segment sizes and offsets after the header
+  uint32_t *d_seg_off = nullptr;
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
-  uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr;  // optimal
+  uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;  // optimal
   uint32_t *d_syms = nullptr, *d_symn = nullptr;  // optimal: per block, the symbols the counting pass saw
   uint8_t *d_dht = nullptr;
   int16_t *d_dbg = nullptr;
-  uint64_t *h_sizes = nullptr;   // page-locked: frame offsets [0, n] of the submit (k_stuff)
+  uint64_t *h_sizes = nullptr;
   uint32_t *h_status = nullptr;
-  std::vector<uint64_t> sizes;   // frame sizes, from h_sizes at sync
-  uint64_t *d_lb = nullptr;      // k_stuff's look-back words, one per tile of chunk groups
-  uint32_t epoch = 0;            // k_stuff launch tag of this slot (1 .. kMaxEpoch)
   hipEvent_t done = nullptr, enc_done = nullptr;
   hipEvent_t ev[MJG_NUM_KERNELS][2] = {};
 };
@@ -251,9 +250,9 @@ void free_ctx(mjg_ctx *c) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
-    void *sp[] = {S.d_scratch, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, S.d_status,
-                  S.d_frame_offsets, S.d_out, S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_dht, S.d_dbg, S.d_syms, S.d_symn,
-                  S.d_lb};
+    void *sp[] = {S.d_scratch, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+                  S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_out,
+                  S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg, S.d_syms, S.d_symn};
     for (void *p : sp)
       if (p) (void)hipFree(p);
     if (S.h_sizes) (void)hipHostFree(S.h_sizes);
@@ -397,19 +396,19 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   int rc;
   if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&S.d_chunk_bits, B * NC)) || (rc = dmalloc(&S.d_chunk_off, B * NC)) ||
+      (rc = dmalloc(&S.d_group_ff, B * NC)) || (rc = dmalloc(&S.d_ff_off, B * NC)) ||
       (rc = dmalloc(&S.d_frame_bits, B * NS)) || (rc = dmalloc(&S.d_status, 4)) ||
-      (rc = dmalloc(&S.d_frame_offsets, B + 1)) ||
-      (rc = dmalloc(&S.d_work, (size_t)(kXcds + 1) * kCtrStride)) || (rc = dmalloc(&S.d_lb, B * NC)))
+      (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)) ||
+      (rc = dmalloc(&S.d_work, (size_t)kXcds * kCtrStride)))
     return rc;
-  // k_encode's unit counters [0, kXcds), k_stuff's ticket at kXcds (reset by k_scan_bits)
-  HIP_TRY(hipMemset(S.d_work, 0, (size_t)(kXcds + 1) * kCtrStride * sizeof(uint32_t)));
-  HIP_TRY(hipMemset(S.d_lb, 0, B * NC * sizeof(uint64_t)));
+  HIP_TRY(hipMemset(S.d_work, 0, (size_t)kXcds * kCtrStride * sizeof(uint32_t)));
+  if (c->rst && ((rc = dmalloc(&S.d_seg_size, B * NS)) || (rc = dmalloc(&S.d_seg_off, B * NS)))) return rc;
   S.out_cap = B * (c->enc_frame_bytes + c->hdr.size() + 4096 + 2 * NS);
   if ((rc = dmalloc(&S.d_out, S.out_cap))) return rc;
   if (c->optimal &&
       ((rc = dmalloc(&S.d_hist, B * kFrameTabWords)) || (rc = dmalloc(&S.d_ftabs, B * kFrameTabWords)) ||
        (rc = dmalloc(&S.d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&S.d_dht_nval, B * 4)) ||
-       (rc = dmalloc(&S.d_syms, B * NC * (size_t)kSymCap * 64)) ||
+       (rc = dmalloc(&S.d_hdr_lens, B)) || (rc = dmalloc(&S.d_syms, B * NC * (size_t)kSymCap * 64)) ||
        (rc = dmalloc(&S.d_symn, B * NC * 64))))
     return rc;
   if (g.debug_coefs && (rc = dmalloc(&S.d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
@@ -790,29 +789,25 @@ void tmark(mjg_ctx *c, Slot &S, int k, int end) {
   (void)hipEventRecord(S.ev[k][end], tail ? c->tail : c->stream);
 }
 
-// The stuffing tail after k_scan_bits: k_stuff (one pass: 0xFF counts, look-back offsets,
-// header, stuffed scan, RSTn / EOI), then the frame offsets and the overflow flag to the host.
-// rerun (the regrow path): the overflow flag and k_stuff's ticket are reset first (a submit's
-// k_scan_bits resets both).
-constexpr uint32_t kMaxEpoch = (1u << 20) - 1;  // k_stuff look-back tags (kLbValueBits + 2 + 20 = 64)
-int launch_write(mjg_ctx *c, Slot &S, int n, bool rerun) {
+// status: reset the overflow flag first (the regrow path; a submit's scan kernel resets it)
+int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
   const EncGeom &g = c->geom;
-  const int gps = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gps * n * g.nseg;
-  if (rerun) {
-    HIP_TRY(hipMemsetAsync(S.d_status, 0, 4, c->tail));
-    HIP_TRY(hipMemsetAsync(S.d_work + kXcds * kCtrStride, 0, 4, c->tail));
-  }
-  S.epoch = S.epoch % kMaxEpoch + 1;
-  if (S.epoch == 1) HIP_TRY(hipMemsetAsync(S.d_lb, 0, (size_t)ngroups * sizeof(uint64_t), c->tail));
+  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n * g.nseg;
+  if (reset_status) HIP_TRY(hipMemsetAsync(S.d_status, 0, 4, c->tail));
   tmark(c, S, MJG_K_WRITE, 0);
-  k_stuff<<<(ngroups + kStuffTile - 1) / kStuffTile, 64 * kStuffWaves, 0, c->tail>>>(
-      S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, g.nchunks, gps, ngroups, g.nseg, c->d_hdr,
-      (int)c->hdr.size(), c->optimal ? S.d_dht_nval : nullptr, (int)c->dht_pos, (int)c->dht_end, S.d_dht, S.d_out,
-      (uint64_t)S.out_cap, S.d_frame_offsets, S.d_status, S.d_lb, S.epoch, S.d_work + kXcds * kCtrStride);
+  k_frame_hdr<<<n, 64, 0, c->tail>>>(S.d_frame_size, c->d_hdr, (int)c->hdr.size(), S.d_out,
+                                       (uint64_t)S.out_cap, S.d_frame_offsets, S.d_status,
+                                       c->optimal ? S.d_hdr_lens : nullptr, (int)c->dht_pos,
+                                       (int)c->dht_end, S.d_dht, S.d_dht_nval, S.d_seg_off,
+                                       S.d_seg_size, g.nseg);
+  k_write<<<(ngroups + 3) / 4, 256, 0, c->tail>>>(
+      S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, S.d_ff_off, S.d_frame_size,
+      S.d_frame_offsets, (int)c->hdr.size(), c->optimal ? S.d_hdr_lens : nullptr, g.nchunks, gpf,
+      ngroups, S.d_out, (uint64_t)S.out_cap, S.d_seg_off, g.nseg);
   tmark(c, S, MJG_K_WRITE, 1);
-  if (c->timing && !c->timing_detail && !rerun) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->tail);
+  if (c->timing && !c->timing_detail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->tail);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(S.h_sizes, S.d_frame_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+  HIP_TRY(hipMemcpyAsync(S.h_sizes, S.d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
                          c->tail));
   HIP_TRY(hipMemcpyAsync(S.h_status, S.d_status, 4, hipMemcpyDeviceToHost, c->tail));
   HIP_TRY(hipEventRecord(S.done, c->tail));
@@ -1032,6 +1027,27 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
                                            S.d_work, S.d_status);
   tmark(c, S, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
+  tmark(c, S, MJG_K_COUNT_FF, 0);
+  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
+  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_scratch, S.d_chunk_bits, S.d_chunk_off,
+                                                           S.d_frame_bits, S.d_group_ff, g.nchunks,
+                                                           gpf, gpf * nsegs);
+  tmark(c, S, MJG_K_COUNT_FF, 1);
+  HIP_TRY(hipGetLastError());
+  tmark(c, S, MJG_K_SCAN_FF, 0);
+  // optimal: header = default header - its 348 table values + the frame's
+  if (c->rst) {  // segment sizes (each with its RSTn / EOI trailer), then per-frame offsets
+    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+                                                          S.d_seg_size, gpf, nsegs);
+    k_seg_sizes<<<n, 64, 0, c->tail>>>(S.d_seg_size, g.nseg, (int)c->hdr.size(), S.d_seg_off,
+                                         S.d_frame_size);
+  } else {
+    k_scan_ff<<<n, 1024, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, S.d_frame_size,
+                                         gpf, (int)c->hdr.size(), c->optimal ? S.d_dht_nval : nullptr,
+                                         (int)c->hdr.size() - 348, S.d_hdr_lens);
+  }
+  tmark(c, S, MJG_K_SCAN_FF, 1);
+  HIP_TRY(hipGetLastError());
   int rc = launch_write(c, S, n, false);
   if (rc) return rc;
   S.n = n;
@@ -1052,8 +1068,9 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
     Slot &S = c->slot[si];
     HIP_TRY(hipEventSynchronize(S.done));
     const int n = S.n;
-    uint64_t t = S.h_sizes[n];  // frame offsets [0, n]: complete even when the output overflowed
-    if (*S.h_status & 1u) {  // packed output overflowed: grow, re-run the stuffing pass only
+    uint64_t t = 0;
+    for (int i = 0; i < n; i++) t += S.h_sizes[i];
+    if (*S.h_status & 1u) {  // packed output overflowed: grow, re-run the write pass only
       HIP_TRY(hipFree(S.d_out));
       S.d_out = nullptr;
       S.out_cap = t + t / 4 + 4096;
@@ -1074,8 +1091,6 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
       }
       c->t_n++;
     }
-    S.sizes.resize(n);
-    for (int i = 0; i < n; i++) S.sizes[i] = S.h_sizes[i + 1] - S.h_sizes[i];
     S.total = t;
     S.pending = false;
     c->nout--;
@@ -1083,7 +1098,7 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
   }
   c->synced_since_submit = true;
   const Slot &L = c->slot[c->last];
-  if (frame_sizes) memcpy(frame_sizes, L.sizes.data(), L.n * sizeof(uint64_t));
+  if (frame_sizes) memcpy(frame_sizes, L.h_sizes, L.n * sizeof(uint64_t));
   if (total) *total = L.total;
   return MJG_OK;
 }

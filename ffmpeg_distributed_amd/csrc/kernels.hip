@@ -1601,7 +1601,7 @@ __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk
                                                     uint32_t *__restrict__ work_ctr,
                                                     uint32_t *__restrict__ status) {
   const int f = blockIdx.x;
-  if (f == 0 && threadIdx.x <= kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;  // k_encode's unit counters, k_stuff's ticket
+  if (f == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;  // k_encode's unit counters
   if (f == 0 && threadIdx.x == 0) *status = 0;  // output overflow flag, set by k_stuff
   uint32_t *cb = chunk_bits + (size_t)f * nchunks;
   for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
@@ -1630,7 +1630,7 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
                                                        int nsegs, uint32_t *__restrict__ work_ctr,
                                                        uint32_t *__restrict__ status) {
   const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x <= kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *status = 0;
   if (sg >= nsegs) return;
   uint32_t *cb = chunk_bits + (size_t)sg * nchunks;
@@ -1739,222 +1739,206 @@ __device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t t
   return n;
 }
 
-// ----------------------------------------------------------------- k_stuff
-// The whole stuffing tail in one launch: replaces k_count_ff -> k_scan_ff (-> k_scan_ff_seg,
-// k_seg_sizes) -> k_frame_hdr -> k_write.  A workgroup takes a *tile* of kStuffTile
-// consecutive groups of kChunksPerWave chunks in submit order (frame, entropy-coded segment,
-// group) by ticket, so every smaller tile is already held by a running workgroup:
-//   1. each wave takes every kStuffWaves-th group of the tile: its owned words (realigned to the
-//      segment's bit offsets from k_scan_bits, the last byte padded with 1s) and their 0xFF
-//      count give the group's byte count A = owned bytes + 0xFFs (+ the frame header for a
-//      frame's first group, + the 2-byte RSTn / EOI trailer for a segment's last group);
-//   2. a scan of the tile's counts in LDS gives each group's offset in the tile and the
-//      tile's total, which is published at once (one 8-byte word: launch epoch, flag, value);
-//   3. decoupled look-back over the tiles before it: the exclusive prefix P is the sum of the
-//      published totals down to the nearest published inclusive prefix, then P + total is
-//      published as the tile's inclusive prefix;
-//   4. each wave writes its groups again: header (first group of a frame), stuffed bytes
-//      (ff_mjpeg_escape_FF) and trailer (mjpegenc.c ff_mjpeg_encode_stuffing RST0 + (mb_y & 7),
-//      then EOI) at P + the group's offset; a frame's last group stores the frame's end
-//      offset (frame_offsets[f + 1]).
-// Tiles, not single groups, take part in the look-back: with ~45K groups per 120-frame 4K
-// submit in flight together, a look-back per group propagated the inclusive prefixes 64 groups
-// per poll round (measured: 0.58 ms for the launch); per tile of 64 groups the chain is 64x
-// shorter.  A group whose bytes would pass out_cap writes nothing and sets status bit 0; the
-// offsets are complete either way, so the host regrows the output to frame_offsets[n] and
-// runs the pass again.  Every workgroup publishes its total before it waits on anything: no
-// workgroup waits on one that waits on it, whatever the placement.
-constexpr int kStuffTile = 64;    // groups per workgroup
-constexpr int kStuffWaves = 16;  // waves per workgroup (kStuffTile / kStuffWaves groups each)
-constexpr int kLbValueBits = 42;
-__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint32_t flag, uint64_t v) {
-  return ((uint64_t)epoch << (kLbValueBits + 2)) | ((uint64_t)flag << kLbValueBits) | v;
-}
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+__global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
+                                                  const uint32_t *__restrict__ chunk_bits,
+                                                  const uint32_t *__restrict__ chunk_off,
+                                                  const uint32_t *__restrict__ frame_bits,
+                                                  uint32_t *__restrict__ group_ff, int nchunks,
+                                                  int ngroups_per_frame, int ngroups) {
+  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (gi >= ngroups) return;
+  const GroupWords g =
+      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
+  int cnt = 0;
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
+    WordLoad ld[kWordsPerLane];
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v += (uint64_t)__shfl_xor((long long)v, d, 64);
-  return v;
-}
-
-// Frame header bytes [0, hl) at fo: the context's header, or with -huffman optimal its bytes
-// before and after the DHT around the frame's own DHT (jpeg_table_header: one DHT, tables DC0,
-// DC1, AC0, AC1).
-__device__ __forceinline__ void write_frame_header(uint8_t *fo, int f, int lane, const uint8_t *hdr, int hdr_len,
-                                                   const uint32_t *dht_nval, int dht_pos, int dht_end,
-                                                   const uint8_t *dht) {
-  if (!dht_nval) {
-    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
-    return;
-  }
-  const uint32_t *nv = dht_nval + 4 * (size_t)f;
-  const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
-  for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
-  uint8_t *o = fo + dht_pos;
-  if (lane == 0) {
-    o[0] = 0xff;
-    o[1] = 0xc4;
-    o[2] = (uint8_t)(len >> 8);
-    o[3] = (uint8_t)len;
-  }
-  o += 4;
-  for (int t = 0; t < 4; t++) {
-    const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
-    const int n = 16 + (int)nv[t];
-    if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
-    for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
-    o += 1 + n;
-  }
-  const int tail = hdr_len - dht_end;
-  for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
-}
-
-// One round of a group's words: lane i holds words kb + 64 j + lane (j < kWordsPerLane).
-struct StuffRound {
-  uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
-};
-
-__device__ __forceinline__ void stuff_round(const GroupWords &g, uint32_t kb, int lane, StuffRound &r) {
-  WordLoad ld[kWordsPerLane];
+    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
+    uint32_t v[kWordsPerLane];
 #pragma unroll
-  for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
+    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
 #pragma unroll
-  for (int i = 0; i < kWordsPerLane; i++) {
-    const uint32_t k = kb + 64 * i + lane;
-    r.v[i] = word_value(g, ld[i], min(k, g.k1 - 1));
-    r.cnt[i] = k < g.k1 ? (uint32_t)ff_in_word(r.v[i], 4 * k, g.total_bytes) : 0u;
-  }
-}
-
-// Stuffed bytes of one round at base (+ carry: 0xFFs of the group's earlier rounds).
-__device__ __forceinline__ void stuff_write(const GroupWords &g, uint32_t kb, int lane, const StuffRound &r,
-                                            uint8_t *base, uint32_t &carry) {
-#pragma unroll
-  for (int i = 0; i < kWordsPerLane; i++) {
-    const uint32_t k = kb + 64 * i + lane;
-    const uint32_t incl = wave_incl_scan(r.cnt[i], lane);
-    if (k < g.k1) {
-      uint8_t *p = base + 4 * (k - g.k0) + carry + incl - r.cnt[i];
-#pragma unroll
-      for (int bb = 0; bb < 4; bb++) {
-        if (4 * k + bb < g.total_bytes) {
-          const uint8_t byte = (uint8_t)(r.v[i] >> (24 - 8 * bb));
-          *p++ = byte;
-          if (byte == 0xff) *p++ = 0;
-        }
-      }
+    for (int i = 0; i < kWordsPerLane; i++) {
+      const uint32_t k = kb + 64 * i + lane;
+      if (k < g.k1) cnt += ff_in_word(v[i], 4 * k, g.total_bytes);
     }
+  }
+  cnt = wave_sum(cnt);
+  if (lane == 0) group_ff[gi] = (uint32_t)cnt;
+}
+
+// Per frame: exclusive scan of the chunk groups' 0xFF counts -> stuffed frame size.
+// -huffman optimal (dht_nval != null): the header length is per frame, hdr_base plus the
+// frame's table values, stored to hdr_lens for k_frame_hdr / k_write.
+__global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ group_ff,
+                                                  uint32_t *__restrict__ ff_off,
+                                                  const uint32_t *__restrict__ frame_bits,
+                                                  uint64_t *__restrict__ frame_size, int ngroups_per_frame,
+                                                  int hdr_len, const uint32_t *__restrict__ dht_nval,
+                                                  int hdr_base, uint32_t *__restrict__ hdr_lens) {
+  const int f = blockIdx.x;
+  const size_t g0 = (size_t)f * ngroups_per_frame;
+  const uint32_t t = block_excl_scan(group_ff + g0, ff_off + g0, ngroups_per_frame);
+  if (threadIdx.x == 0) {
+    uint32_t hl = (uint32_t)hdr_len;
+    if (dht_nval) {
+      hl = (uint32_t)hdr_base + dht_nval[4 * f] + dht_nval[4 * f + 1] + dht_nval[4 * f + 2] +
+           dht_nval[4 * f + 3];
+      hdr_lens[f] = hl;
+    }
+    frame_size[f] = (uint64_t)hl + ((frame_bits[f] + 7) >> 3) + t + 2;
+  }
+}
+
+// RST mode, per segment (wave): scan of its groups' 0xFF counts -> stuffed segment size
+// including the 2-byte trailer (RSTn or, for the frame's last segment, EOI).
+__global__ __launch_bounds__(256) void k_scan_ff_seg(const uint32_t *__restrict__ group_ff,
+                                                     uint32_t *__restrict__ ff_off,
+                                                     const uint32_t *__restrict__ seg_bits,
+                                                     uint64_t *__restrict__ seg_size, int ngroups_per_seg,
+                                                     int nsegs) {
+  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (sg >= nsegs) return;
+  const size_t g0 = (size_t)sg * ngroups_per_seg;
+  const uint32_t t = wave_excl_scan_arr(group_ff + g0, ff_off + g0, ngroups_per_seg, lane);
+  if (lane == 0) seg_size[sg] = (uint64_t)((seg_bits[sg] + 7) >> 3) + t + 2;
+}
+
+// RST mode (one entropy-coded segment per MCU row): per frame, the segments' offsets after
+// the header (exclusive scan of their stuffed sizes, each including its 2-byte trailer:
+// RSTn, or EOI for the last) and the frame size = header + all segments.
+__global__ __launch_bounds__(64) void k_seg_sizes(const uint64_t *__restrict__ seg_size, int nseg,
+                                                  int hdr_len, uint32_t *__restrict__ seg_off,
+                                                  uint64_t *__restrict__ frame_size) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  uint32_t carry = 0;
+  for (int s0 = 0; s0 < nseg; s0 += 64) {
+    const int s = s0 + lane;
+    const uint32_t v = s < nseg ? (uint32_t)seg_size[(size_t)f * nseg + s] : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (s < nseg) seg_off[(size_t)f * nseg + s] = carry + incl - v;
     carry += lane63(incl);
   }
+  if (lane == 0) frame_size[f] = (uint64_t)hdr_len + carry;
 }
 
-__global__ __launch_bounds__(64 * kStuffWaves) void k_stuff(
-    const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
-    const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ seg_bits, int nchunks, int gps,
-    int ngroups, int nseg, const uint8_t *__restrict__ hdr, int hdr_len,
-    const uint32_t *__restrict__ dht_nval, int dht_pos, int dht_end, const uint8_t *__restrict__ dht,
-    uint8_t *__restrict__ out, uint64_t out_cap, uint64_t *__restrict__ frame_offsets,
-    uint32_t *__restrict__ status, uint64_t *__restrict__ lb, uint32_t epoch, uint32_t *__restrict__ ticket) {
-  __shared__ uint32_t s_cnt[kStuffTile], s_off[kStuffTile];  // group byte counts, offsets in the tile
-  __shared__ uint64_t s_base;             // the tile's exclusive prefix
-  __shared__ int s_tile;
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  if (tid == 0) s_tile = (int)atomicAdd(ticket, 1u);
-  __syncthreads();
-  const int tile = s_tile;
-  const int g0 = tile * kStuffTile;
-  if (g0 >= ngroups) return;  // (uniform over the workgroup)
-  const int ng = min(kStuffTile, ngroups - g0);
-  auto header_len = [&](int fr) {
-    uint32_t hl = (uint32_t)hdr_len;
-    if (dht_nval) {  // -huffman optimal: the default header's 348 table values -> the frame's
-      const uint32_t *nv = dht_nval + 4 * (size_t)fr;
-      hl = (uint32_t)hdr_len - 348u + nv[0] + nv[1] + nv[2] + nv[3];
-    }
-    return hl;
-  };
-  // 1. the byte count of each group of the tile
-  for (int k = wave; k < ng; k += kStuffWaves) {
-    const GroupWords g = group_words(scratch, chunk_bits, chunk_off, seg_bits, nchunks, gps, g0 + k, lane);
-    const int fr = g.f / nseg, sif = g.f - fr * nseg;
-    uint32_t ff = 0;
-    for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
-      StuffRound r;
-      stuff_round(g, kb, lane, r);
+// One wave per frame: packed output offset (sum of the preceding frame sizes), capacity
+// check, header (SOI .. SOS) and EOI of the frame; in RST mode (seg_off != null) also the
+// RST0..7 marker closing every segment but the last (mjpegenc.c ff_mjpeg_encode_stuffing:
+// RST0 + (mb_y & 7) after MCU row mb_y).  -huffman optimal (hdr_lens != null):
+// the default header's bytes before and after its DHT around the frame's own DHT
+// (jpeg_table_header: one DHT, tables DC0, DC1, AC0, AC1).
+__global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ frame_size,
+                                                  const uint8_t *__restrict__ hdr, int hdr_len,
+                                                  uint8_t *__restrict__ out, uint64_t out_cap,
+                                                  uint64_t *__restrict__ frame_offsets,
+                                                  uint32_t *__restrict__ status,
+                                                  const uint32_t *__restrict__ hdr_lens, int dht_pos,
+                                                  int dht_end, const uint8_t *__restrict__ dht,
+                                                  const uint32_t *__restrict__ dht_nval,
+                                                  const uint32_t *__restrict__ seg_off,
+                                                  const uint64_t *__restrict__ seg_size, int nseg) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  uint64_t s = 0;
+  for (int i = lane; i < f; i += 64) s += frame_size[i];
 #pragma unroll
-      for (int i = 0; i < kWordsPerLane; i++) ff += r.cnt[i];
-    }
-    ff = (uint32_t)wave_sum((int)ff);
-    const uint32_t owned = min(4 * g.k1, g.total_bytes) - min(4 * g.k0, g.total_bytes);
-    const bool first = sif == 0 && g.c0 == 0, last = g.c0 + kChunksPerWave >= nchunks;
-    if (lane == 0) s_cnt[k] = owned + ff + (first ? header_len(fr) : 0u) + (last ? 2u : 0u);
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  const uint64_t fsize = frame_size[f];
+  if (lane == 0) {
+    frame_offsets[f] = s;
+    if (f == (int)gridDim.x - 1) frame_offsets[f + 1] = s + fsize;
   }
-  __syncthreads();
-  // 2./3. the tile's offsets and total; look-back for its prefix
-  if (wave == 0) {
-    const uint32_t a = lane < ng ? s_cnt[lane] : 0u;
-    const uint32_t incl = wave_incl_scan(a, lane);
-    const uint64_t total = lane63(incl);
-    if (lane < ng) s_off[lane] = incl - a;
-    if (lane == 0)
-      __hip_atomic_store(lb + tile, lb_word(epoch, tile == 0 ? 2u : 1u, total), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    constexpr uint64_t kVal = (1ull << kLbValueBits) - 1;
-    for (int end = tile; end > 0; end -= 64) {
-      const int j = end - 1 - lane;  // lane 0: the nearest predecessor
-      uint64_t w, incl_mask;
-      while (true) {
-        w = j >= 0 ? __hip_atomic_load(lb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : lb_word(epoch, 2u, 0);
-        const uint32_t fl = (uint32_t)(w >> kLbValueBits) & 3u;
-        const bool ready = (uint32_t)(w >> (kLbValueBits + 2)) == epoch && fl != 0;
-        incl_mask = __ballot(ready && fl == 2u);
-        const uint64_t waiting = __ballot(!ready);
-        // usable when every predecessor up to the nearest inclusive prefix (or the whole
-        // window) has published
-        const uint64_t need = incl_mask ? ((incl_mask & (~incl_mask + 1)) << 1) - 1 : ~0ull;
-        if (!(waiting & need)) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      const int stop = incl_mask ? (int)__builtin_ctzll(incl_mask) : 63;
-      excl += wave_sum64(lane <= stop ? (w & kVal) : 0ull);
-      if (incl_mask) break;
-    }
+  if (s + fsize > out_cap) {
+    if (lane == 0) atomicOr(status, 1u);
+    return;
+  }
+  uint8_t *fo = out + s;
+  if (!hdr_lens) {
+    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
+  } else {
+    const uint32_t *nv = dht_nval + 4 * (size_t)f;
+    const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
+    for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
+    uint8_t *o = fo + dht_pos;
     if (lane == 0) {
-      if (tile > 0)
-        __hip_atomic_store(lb + tile, lb_word(epoch, 2u, excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        frame_offsets[0] = 0;
-      s_base = excl;
+      o[0] = 0xff;
+      o[1] = 0xc4;
+      o[2] = (uint8_t)(len >> 8);
+      o[3] = (uint8_t)len;
     }
+    o += 4;
+    for (int t = 0; t < 4; t++) {
+      const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
+      const int n = 16 + (int)nv[t];
+      if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
+      for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
+      o += 1 + n;
+    }
+    const int tail = hdr_len - dht_end;
+    for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
   }
-  __syncthreads();
-  // 4. write
-  const uint64_t base = s_base;
-  for (int k = wave; k < ng; k += kStuffWaves) {
-    const GroupWords g = group_words(scratch, chunk_bits, chunk_off, seg_bits, nchunks, gps, g0 + k, lane);
-    const int fr = g.f / nseg, sif = g.f - fr * nseg;
-    const bool first = sif == 0 && g.c0 == 0, last = g.c0 + kChunksPerWave >= nchunks;
-    const uint64_t p0 = base + s_off[k], pend = p0 + s_cnt[k];
-    const uint32_t hl = first ? header_len(fr) : 0u;
-    if (last && sif == nseg - 1 && lane == 0) frame_offsets[fr + 1] = pend;
-    if (pend > out_cap) {
-      if (lane == 0) atomicOr(status, 1u);
-      continue;
-    }
-    uint8_t *o = out + p0;
-    if (first) write_frame_header(o, fr, lane, hdr, hdr_len, dht_nval, dht_pos, dht_end, dht);
-    o += hl;
-    uint32_t carry = 0;
-    for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
-      StuffRound r;
-      stuff_round(g, kb, lane, r);
-      stuff_write(g, kb, lane, r, o, carry);
-    }
-    if (last && lane == 0) {
-      uint8_t *m = out + pend - 2;
+  if (lane == 0) {
+    fo[fsize - 2] = 0xff;
+    fo[fsize - 1] = 0xd9;
+  }
+  if (seg_off)
+    for (int sg = lane; sg < nseg - 1; sg += 64) {
+      const size_t i = (size_t)f * nseg + sg;
+      uint8_t *m = fo + hdr_len + seg_off[i] + seg_size[i] - 2;
       m[0] = 0xff;
-      m[1] = sif == nseg - 1 ? 0xd9 : (uint8_t)(0xd0 + (sif & 7));
+      m[1] = (uint8_t)(0xd0 + (sg & 7));
+    }
+}
+
+// Wave per chunk group, lanes = words: the group's owned bytes with a 0x00 after every
+// 0xFF (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs before it in the
+// frame (group prefix from k_scan_ff, in-group prefix by a wave scan).
+__global__ __launch_bounds__(256) void k_write(
+    const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
+    const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
+    const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
+    const uint64_t *__restrict__ frame_offsets, int hdr_len, const uint32_t *__restrict__ hdr_lens,
+    int nchunks, int ngroups_per_frame, int ngroups, uint8_t *__restrict__ out, uint64_t out_cap,
+    const uint32_t *__restrict__ seg_off, int nseg) {
+  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (gi >= ngroups) return;
+  // g.f is the entropy-coded segment (the frame itself unless RST mode)
+  const GroupWords g =
+      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
+  const int fr = g.f / nseg;
+  const uint64_t foff = frame_offsets[fr];
+  if (foff + frame_size[fr] > out_cap) return;  // k_frame_hdr flagged the overflow
+  const uint32_t hl = hdr_lens ? hdr_lens[fr] : (uint32_t)hdr_len;
+  uint8_t *base = out + foff + hl + (seg_off ? seg_off[g.f] : 0u) + 4 * (size_t)g.k0 + ff_off[gi];
+  uint32_t carry = 0;
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
+    WordLoad ld[kWordsPerLane];
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
+    uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) {
+      const uint32_t k = kb + 64 * i + lane;
+      cnt[i] = k < g.k1 ? (uint32_t)ff_in_word(v[i], 4 * k, g.total_bytes) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kWordsPerLane; i++) {
+      const uint32_t k = kb + 64 * i + lane;
+      const uint32_t incl = wave_incl_scan(cnt[i], lane);
+      if (k < g.k1) {
+        uint8_t *p = base + 4 * (k - g.k0) + carry + incl - cnt[i];
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+          if (4 * k + bb < g.total_bytes) {
+            const uint8_t byte = (uint8_t)(v[i] >> (24 - 8 * bb));
+            *p++ = byte;
+            if (byte == 0xff) *p++ = 0;
+          }
+        }
+      }
+      carry += lane63(incl);
     }
   }
 }

@@ -58,9 +58,9 @@ extern "C" {
 #define MJG_CHROMA_422 1       /* yuv(j)422p: MCU 16x16, Y 2x2 Cb 1x2 Cr 1x2 */
 #define MJG_CHROMA_444 2       /* yuv(j)444p: MCU 8x16, every component 1x2 (ff_mjpeg_init_hvsample) */
 
-#define MJG_F_TIMING_DETAIL 64u /* MJG_F_TIMING plus events around each tail kernel (k_scan_bits:
-                                  MJG_K_SCAN_BITS, k_stuff: MJG_K_WRITE); each event adds ~10 us
-                                  of GPU idle between those short kernels */
+#define MJG_F_TIMING_DETAIL 64u /* MJG_F_TIMING plus events around every tail kernel (scan, 0xFF
+                                  count, write: MJG_K_SCAN_BITS .. MJG_K_WRITE); each event adds
+                                  ~10 us of GPU idle between those short kernels */
 #define MJG_F_FUSED 128u       /* with -vf scale: scale and encode in one kernel, k_scale_encode
                                   (scaled pixels kept in LDS, never in HBM) instead of k_scale
                                   (scaled frames to HBM) + k_encode.  Same bytes.  Opt-in: on
@@ -79,10 +79,9 @@ extern "C" {
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */
 #define MJG_K_ENCODE 1         /* load [+ fused scale] + FDCT + quant + Huffman -> chunk bits */
 #define MJG_K_SCAN_BITS 2      /* per-frame exclusive scan of chunk bit lengths      */
-#define MJG_K_COUNT_FF 3       /* (since r03 part of k_stuff: always 0)              */
-#define MJG_K_SCAN_FF 4        /* (since r03 part of k_stuff: always 0)              */
-#define MJG_K_WRITE 5          /* k_stuff: realign, pad, count 0xFF, look back for the output
-                                  offset, header + stuffed scan + RSTn / EOI          */
+#define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk      */
+#define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes        */
+#define MJG_K_WRITE 5          /* header + stuffed scan + EOI into packed output     */
 #define MJG_K_HUFF 6           /* -huffman optimal: symbol-count pass + table build   */
 #define MJG_K_TAIL 7           /* MJG_K_SCAN_BITS .. MJG_K_WRITE as one interval (MJG_F_TIMING) */
 #define MJG_NUM_KERNELS 8

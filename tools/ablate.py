@@ -11,8 +11,6 @@ build are wrong by construction; only kernel times (and SQ counters) are compare
   noexact  : exact_coef returns a constant (the candidate loop and coding kept)
   noscreen : column screen skipped (DC from the row image, no candidates): loads + row pass +
              DC/EOB coding + pack
-  stuff_w4, stuff_w8, stuff_t32: k_stuff with 4 / 8 waves per workgroup, or 32-group tiles
-             (same bytes; for the tail's shape A/B)
   nodct    : row pass and column screen skipped (raw rows copied into the LDS image): loads +
              LDS image + DC/EOB coding + pack
 
@@ -34,14 +32,7 @@ EXACT = "  const int ro = n >> 3, c = n & 7;\n  const uint32_t sel = (c & 1) ? 0
 SCREEN = "      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);"
 ROWPASS = "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);"
 
-TILE = "constexpr int kStuffTile = 64;    // groups per workgroup"
-WAVES = "constexpr int kStuffWaves = 16;  // waves per workgroup (kStuffTile / kStuffWaves groups each)"
-
 SUBS = {
-    # k_stuff shape (not ablations: same bytes)
-    "stuff_w4": [(WAVES, WAVES.replace("16", "4", 1))],
-    "stuff_w8": [(WAVES, WAVES.replace("16", "8", 1))],
-    "stuff_t32": [(TILE, TILE.replace("64", "32", 1))],
     "noemit": [(EMIT, "      q.emit(((uint32_t)__popcll(mask) << 8) ^ ((uint32_t)diff & 255u), 16);\n"),
                (WIDE, "const uint64_t wide = 0;")],
     "noexact": [(EXACT, "  if (n >= 0) return 1 + (n & 1);\n" + EXACT)],

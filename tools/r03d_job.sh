@@ -2,7 +2,7 @@
 # round 3 job (tiled k_stuff): GPU tests on the in-tree build; kernel A/B against the round-2
 # code (libmjgpu_v_oldtail.so) and the phase ablations (tools/ablate.py) in one process; bench
 # A/B old vs new; default bench line with the e2e leg.
-#   Usage: [V2=... V1=...] bash tools/r03d_job.sh TAG  (V2/V1: the c2/c1 VARIANTS)
+#   Usage: [V2=... V1=...] [PROF=1] bash tools/r03d_job.sh TAG  (V2/V1: the c2/c1 VARIANTS)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -26,4 +26,5 @@ done
 unset MJG_LIBRARY
 timeout -k 10 300 python bench.py --cpu-seconds 2 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], json.dumps(d['kernel_ms_per_step'])); print(json.dumps(d['e2e']))"
+if [ -n "$PROF" ]; then bash tools/driver_prof.sh $1/driver || exit $?; fi
 echo done
