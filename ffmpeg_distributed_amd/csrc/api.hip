@@ -176,12 +176,14 @@ struct Slot {
   int n = 0;
   uint64_t total = 0;
   uint32_t *d_scratch = nullptr;
+  uint32_t *d_stream = nullptr;  // k_count_ff's realigned words, per segment (k_write reads them)
   uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
   uint32_t *d_frame_bits = nullptr, *d_status = nullptr;
   uint32_t *d_work = nullptr;  // k_encode's batch counter (zero; reset by the slot's scan kernel)
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
-  uint64_t *d_seg_size = nullptr;  // RST mode: stuffed segment sizes and offsets after the header
+  uint32_t *d_seg_size = nullptr;  // RST mode: stuffed segment sizes and offsets after the header
   uint32_t *d_seg_off = nullptr;
+  uint32_t *d_done = nullptr;      // k_count_ff's tickets: per segment, per frame, one per launch
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
   uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;  // optimal
@@ -250,8 +252,8 @@ void free_ctx(mjg_ctx *c) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
-    void *sp[] = {S.d_scratch, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
-                  S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_out,
+    void *sp[] = {S.d_scratch, S.d_stream, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+                  S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_done, S.d_out,
                   S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg, S.d_syms, S.d_symn};
     for (void *p : sp)
       if (p) (void)hipFree(p);
@@ -395,10 +397,12 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   const EncGeom &g = c->geom;
   int rc;
   if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||
+      (rc = dmalloc(&S.d_stream, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&S.d_chunk_bits, B * NC)) || (rc = dmalloc(&S.d_chunk_off, B * NC)) ||
       (rc = dmalloc(&S.d_group_ff, B * NC)) || (rc = dmalloc(&S.d_ff_off, B * NC)) ||
       (rc = dmalloc(&S.d_frame_bits, B * NS)) || (rc = dmalloc(&S.d_status, 4)) ||
       (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)) ||
+      (rc = dmalloc(&S.d_done, B * NS + B + 1)) ||
       (rc = dmalloc(&S.d_work, (size_t)kXcds * kCtrStride)))
     return rc;
   HIP_TRY(hipMemset(S.d_work, 0, (size_t)kXcds * kCtrStride * sizeof(uint32_t)));
@@ -792,18 +796,14 @@ void tmark(mjg_ctx *c, Slot &S, int k, int end) {
 // status: reset the overflow flag first (the regrow path; a submit's scan kernel resets it)
 int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
   const EncGeom &g = c->geom;
-  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gpf * n * g.nseg;
+  const int gps = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave, ngroups = gps * n * g.nseg;
   if (reset_status) HIP_TRY(hipMemsetAsync(S.d_status, 0, 4, c->tail));
   tmark(c, S, MJG_K_WRITE, 0);
-  k_frame_hdr<<<n, 64, 0, c->tail>>>(S.d_frame_size, c->d_hdr, (int)c->hdr.size(), S.d_out,
-                                       (uint64_t)S.out_cap, S.d_frame_offsets, S.d_status,
-                                       c->optimal ? S.d_hdr_lens : nullptr, (int)c->dht_pos,
-                                       (int)c->dht_end, S.d_dht, S.d_dht_nval, S.d_seg_off,
-                                       S.d_seg_size, g.nseg);
   k_write<<<(ngroups + 3) / 4, 256, 0, c->tail>>>(
-      S.d_scratch, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, S.d_ff_off, S.d_frame_size,
-      S.d_frame_offsets, (int)c->hdr.size(), c->optimal ? S.d_hdr_lens : nullptr, g.nchunks, gpf,
-      ngroups, S.d_out, (uint64_t)S.out_cap, S.d_seg_off, g.nseg);
+      S.d_stream, S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, S.d_ff_off, g.nchunks, gps, g.nseg, n,
+      S.d_seg_size, S.d_seg_off, S.d_frame_offsets, c->d_hdr, (int)c->hdr.size(),
+      c->optimal ? S.d_hdr_lens : nullptr, (int)c->dht_pos, (int)c->dht_end, S.d_dht,
+      c->optimal ? S.d_dht_nval : nullptr, S.d_out, (uint64_t)S.out_cap, S.d_status);
   tmark(c, S, MJG_K_WRITE, 1);
   if (c->timing && !c->timing_detail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->tail);
   HIP_TRY(hipGetLastError());
@@ -1019,33 +1019,28 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   HIP_TRY(hipStreamWaitEvent(c->tail, S.enc_done, 0));
   if (c->timing && !c->timing_detail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->tail);
   tmark(c, S, MJG_K_SCAN_BITS, 0);
+  const int ndone = 1;  // k_scan_ff's frame ticket
   if (c->rst)
     k_scan_bits_seg<<<(nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits,
-                                                            g.nchunks, nsegs, S.d_work, S.d_status);
+                                                            g.nchunks, nsegs, S.d_work, S.d_status, S.d_done,
+                                                            ndone);
   else
     k_scan_bits<<<n, 1024, 0, c->tail>>>(S.d_chunk_bits, S.d_chunk_off, S.d_frame_bits, g.nchunks,
-                                           S.d_work, S.d_status);
+                                           S.d_work, S.d_status, S.d_done, ndone);
   tmark(c, S, MJG_K_SCAN_BITS, 1);
   HIP_TRY(hipGetLastError());
   tmark(c, S, MJG_K_COUNT_FF, 0);
-  const int gpf = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
-  k_count_ff<<<(gpf * nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_scratch, S.d_chunk_bits, S.d_chunk_off,
-                                                           S.d_frame_bits, S.d_group_ff, g.nchunks,
-                                                           gpf, gpf * nsegs);
+  const int gps = (g.nchunks + kChunksPerWave - 1) / kChunksPerWave;
+  k_count_ff<<<(gps * nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_scratch, S.d_chunk_bits, S.d_chunk_off,
+                                                           S.d_frame_bits, S.d_group_ff, g.nchunks, gps,
+                                                           gps * nsegs, S.d_stream);
   tmark(c, S, MJG_K_COUNT_FF, 1);
   HIP_TRY(hipGetLastError());
+  // segment and frame sizes, the frames' packed offsets
   tmark(c, S, MJG_K_SCAN_FF, 0);
-  // optimal: header = default header - its 348 table values + the frame's
-  if (c->rst) {  // segment sizes (each with its RSTn / EOI trailer), then per-frame offsets
-    k_scan_ff_seg<<<(nsegs + 3) / 4, 256, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits,
-                                                          S.d_seg_size, gpf, nsegs);
-    k_seg_sizes<<<n, 64, 0, c->tail>>>(S.d_seg_size, g.nseg, (int)c->hdr.size(), S.d_seg_off,
-                                         S.d_frame_size);
-  } else {
-    k_scan_ff<<<n, 1024, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, S.d_frame_size,
-                                         gpf, (int)c->hdr.size(), c->optimal ? S.d_dht_nval : nullptr,
-                                         (int)c->hdr.size() - 348, S.d_hdr_lens);
-  }
+  k_scan_ff<<<n, 256, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, gps, g.nseg, (int)c->hdr.size(),
+                                      c->optimal ? S.d_dht_nval : nullptr, S.d_hdr_lens, S.d_seg_size,
+                                      S.d_seg_off, S.d_frame_size, S.d_frame_offsets, S.d_done);
   tmark(c, S, MJG_K_SCAN_FF, 1);
   HIP_TRY(hipGetLastError());
   int rc = launch_write(c, S, n, false);

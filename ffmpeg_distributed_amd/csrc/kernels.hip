@@ -9,9 +9,9 @@
 //                 Huffman bit-length pass -> wave prefix-sum -> bit-pack pass into an
 //                 LDS window (ds_or_b32) -> chunk bitstream to a scratch slot
 //   k_scan_bits   per frame: exclusive scan of chunk bit lengths
-//   k_stuff       per group of 8 chunks, one pass: realign the bits to the frame offset, pad
-//                 with 1s, count 0xFF, look back for the packed output offset, then header /
-//                 stuffed scan bytes / RSTn / EOI into the packed output
+//   k_count_ff    per group of 32 chunks: realign the bits to the segment offset, pad with 1s,
+//                 count 0xFF; the last group of a segment / frame / launch sizes and places them
+//   k_write       per group: header / stuffed scan bytes / RSTn / EOI into the packed output
 //
 // Arithmetic follows FFmpeg (see oracle/mjpeg_oracle.c for the per-function citations):
 // libavcodec/jfdctint_template.c, mpegvideo_enc.c dct_quantize_c, mjpegenc.c
@@ -26,7 +26,11 @@ namespace mjg {
 constexpr int kEncWavesPerEU = 3;  // k_encode occupancy target (waves per SIMD); measured best (v8)
 
 constexpr int kMaxBlockBits = 1664;  // >= DC 16 + 63 * (16 + 10) bits
+#ifdef MJG_SLOT_WORDS  // layout experiments only (unsafe below the worst case)
+constexpr int kSlotWords = MJG_SLOT_WORDS;
+#else
 constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 blocks
+#endif
 
 // fp32 exact-integer arithmetic (k_encode): adding kM = 1.5*2^23 rounds to an integer
 // (round-to-nearest-even) and keeps it in the low mantissa bits; kMb = kM + 32768 leaves
@@ -1599,10 +1603,15 @@ __global__ __launch_bounds__(1024) void k_scan_bits(uint32_t *__restrict__ chunk
                                                     uint32_t *__restrict__ chunk_off,
                                                     uint32_t *__restrict__ frame_bits, int nchunks,
                                                     uint32_t *__restrict__ work_ctr,
-                                                    uint32_t *__restrict__ status) {
+                                                    uint32_t *__restrict__ status,
+                                                    uint32_t *__restrict__ done, int ndone) {
   const int f = blockIdx.x;
   if (f == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;  // k_encode's unit counters
-  if (f == 0 && threadIdx.x == 0) *status = 0;  // output overflow flag, set by k_stuff
+  if (f == 0 && threadIdx.x == 0) *status = 0;  // output overflow flag, set by k_write
+  {  // k_count_ff's ticket counters
+    const int i = f * 1024 + (int)threadIdx.x;
+    if (i < ndone) done[i] = 0;
+  }
   uint32_t *cb = chunk_bits + (size_t)f * nchunks;
   for (int i = threadIdx.x; i < nchunks; i += 1024) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
   __syncthreads();
@@ -1628,10 +1637,15 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
                                                        uint32_t *__restrict__ chunk_off,
                                                        uint32_t *__restrict__ seg_bits, int nchunks,
                                                        int nsegs, uint32_t *__restrict__ work_ctr,
-                                                       uint32_t *__restrict__ status) {
+                                                       uint32_t *__restrict__ status,
+                                                       uint32_t *__restrict__ done, int ndone) {
   const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *status = 0;
+  {  // k_count_ff's ticket counters
+    const int i = blockIdx.x * 256 + (int)threadIdx.x;
+    if (i < ndone) done[i] = 0;
+  }
   if (sg >= nsegs) return;
   uint32_t *cb = chunk_bits + (size_t)sg * nchunks;
   for (int i = lane; i < nchunks; i += 64) cb[i] = min(cb[i], (uint32_t)kSlotWords * 32u);
@@ -1639,304 +1653,367 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
   if (lane == 0) seg_bits[sg] = t;
 }
 
-// k_stuff works on *groups* of kChunksPerWave consecutive chunks of an
-// entropy-coded segment (the frame unless RST mode), one wave per group, lanes = the group's
-// words flattened across its chunks.  A word belongs to the chunk holding its first bit, so
-// chunk c owns words [ceil(O_c / 32), ceil(O_{c+1} / 32)) and a group owns one contiguous
-// word range.  Everything per group (offsets, lengths) lives in lane registers, so a word
-// costs only its slot loads, and a round issues all of them before any is used: the pass
-// is load-latency bound (one wave per ~200 words), not bandwidth bound.
-constexpr int kChunksPerWave = 8;
-constexpr int kWordsPerLane = 4;  // words per lane per round
+// ------------------------------------------------------------------ the stuffing tail
+// Three launches after k_scan_bits, on *groups* of kChunksPerWave consecutive chunks of an
+// entropy-coded segment (the frame unless RST mode), one wave per group:
+//   k_count_ff  realigns the group's words to the segment's bit offsets and counts their 0xFF
+//               bytes (group_ff)
+//   k_scan_ff   per frame: scans of the group counts and segment sizes, the frame's size; the
+//               last frame to finish (one ticket per frame) places every frame (frame_offsets)
+//   k_write     the same words again, byte-stuffed (ff_mjpeg_escape_FF): a word without 0xFF
+//               is one (unaligned) dword store; the frame's first group writes the header, a
+//               segment's last group its RSTn / EOI
+// The tail runs beside the next submit's k_encode, whose VALU issue it shares, so its cost per
+// word is kept to a few dozen VALU instructions per 64-word round (group_values).
+#ifndef MJG_TAIL_G
+#define MJG_TAIL_G 32
+#endif
+#ifndef MJG_TAIL_R
+#define MJG_TAIL_R 4
+#endif
+constexpr int kChunksPerWave = MJG_TAIL_G;  // chunks per group (lanes 0..G hold their metadata)
+constexpr int kTailRounds = MJG_TAIL_R;     // 64-word rounds whose slot loads are issued together
+static_assert(kChunksPerWave * kSlotWords < (1 << 17), "group word offsets are 17-bit fields");
 
+// A group: chunks c0 .. c0 + n - 1 of segment s, owning words [k0, k1) of the segment's
+// unstuffed scan (a word belongs to the chunk holding its first bit: chunk c owns
+// [ceil(O_c / 32), ceil(O_{c+1} / 32))).  Lane j < n holds chunk j's packed metadata:
+//   bits  0-16  rsw: its first owned word - k0
+//   bits 17-21  off: 32 * ceil(O / 32) - O, the slot bit where its first owned word starts
+//   bits 22-26  rem - 1: bits of the chunk in its last owned word (1..32)
+//   bit  27     a next chunk exists in the segment
+// lane n: rsw = k1 - k0 (the end of the group's words).
 struct GroupWords {
-  int f, c0, n;          // segment, first chunk, chunks in the group
-  uint32_t T, total_bytes;
-  uint32_t k0, k1;       // owned word range
-  uint32_t o_lane;       // lane j < n: O_{c0+j}; lane n: end offset of the group
-  uint32_t l_lane;       // lane j <= n: L_{c0+j} (lane n: the next group's first chunk, 0 past the segment)
-  const uint32_t *slot0; // scratch slot of chunk c0
-  int nchunks;
+  int s, c0, n;
+  uint32_t T;         // segment bits
+  uint32_t k0, k1;
+  uint32_t info;
+  const uint32_t *slot0;  // scratch slot of chunk c0
 };
 
 __device__ __forceinline__ GroupWords group_words(const uint32_t *scratch, const uint32_t *chunk_bits,
-                                                  const uint32_t *chunk_off, const uint32_t *frame_bits,
-                                                  int nchunks, int ngroups_per_frame, int gi, int lane) {
+                                                  const uint32_t *chunk_off, const uint32_t *seg_bits,
+                                                  int nchunks, int gps, int gi, int lane) {
   GroupWords g;
-  g.f = gi / ngroups_per_frame;
-  g.c0 = (gi - g.f * ngroups_per_frame) * kChunksPerWave;
+  g.s = gi / gps;
+  g.c0 = (gi - g.s * gps) * kChunksPerWave;
   g.n = min(kChunksPerWave, nchunks - g.c0);
-  g.nchunks = nchunks;
-  g.T = frame_bits[g.f];
-  g.total_bytes = (g.T + 7) >> 3;
-  const size_t i0 = (size_t)g.f * nchunks + g.c0;
+  g.T = seg_bits[g.s];
+  const size_t i0 = (size_t)g.s * nchunks + g.c0;
   g.slot0 = scratch + i0 * kSlotWords;
-  g.o_lane = lane < g.n ? chunk_off[i0 + lane] : 0u;
-  g.l_lane = (lane <= g.n && g.c0 + lane < nchunks) ? chunk_bits[i0 + lane] : 0u;
-  const uint32_t last = __shfl(g.o_lane, g.n - 1, 64) + __shfl(g.l_lane, g.n - 1, 64);
-  if (lane == g.n) g.o_lane = last;
-  g.k0 = (__shfl(g.o_lane, 0, 64) + 31) >> 5;
-  g.k1 = (last + 31) >> 5;
+  const uint32_t O = lane < g.n ? chunk_off[i0 + lane] : 0u, L = lane < g.n ? chunk_bits[i0 + lane] : 0u;
+  const uint32_t end = O + L;
+  const uint32_t gend = __builtin_amdgcn_readlane(end, g.n - 1);
+  g.k0 = (__builtin_amdgcn_readfirstlane(O) + 31) >> 5;
+  g.k1 = (gend + 31) >> 5;
+  const uint32_t sw = (O + 31) >> 5, lw = (end + 31) >> 5;  // first owned word, one past the last
+  const uint32_t rem = end - 32 * (lw - 1);                    // 1..32
+  g.info = lane < g.n ? (sw - g.k0) | ((32 * sw - O) << 17) | ((rem - 1) << 22) |
+                            ((uint32_t)(g.c0 + lane + 1 < nchunks) << 27)
+         : lane == g.n ? g.k1 - g.k0 : 0u;
   return g;
 }
 
-// Word k (32 bits, MSB first) of the segment's unstuffed scan, in two steps so a caller can
-// issue the loads of several words before using any: word_load finds the owner chunk c
-// (relative to the group; uniform readlane compares) and loads the three slot words the
-// word can need (independent, unconditional loads), word_value assembles it.  Bits past the
-// chunk come from chunk c+1's first word; past the segment's last bit comes the 1-bit
-// padding to a byte boundary (ff_mjpeg_escape_FF pad).  k must lie in [k0, k1).
-struct WordLoad {
-  uint32_t w0, w1, w2, L, NL, p;
-  bool has_next;
-};
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
 
-__device__ __forceinline__ WordLoad word_load(const GroupWords &g, uint32_t k) {
-  int c = 0;
+// Words kb + 64 i + lane (i < R) of the segment's unstuffed scan, 32 bits MSB first; lanes at
+// or past k1 compute garbage the caller masks (their loads stay inside chunk 0's words).
+//   owner c: the chunk starts inside the window are marked in the wave's LDS bytes; one ballot
+//            per round counts those at or before the lane's word
+//   A:       chunk c's slot word under the word's first bit (every lane); lane + 1's A is the
+//            next slot word of the chunk, or at the chunk's last owned word the next chunk's
+//            first word (it owns word k + 1 from that word's bit 0); lane 63 and the group's last
+//            word load that one themselves (B), and a chunk's last word whose bits span two slot
+//            words loads the second (X), all in the same batch
+//   value:   A:next funnel-shifted by off; at a chunk's last word the next chunk's first bits
+//            follow its rem bits, and past the segment's last bit the 1-bit padding to a byte
+//            boundary (ff_mjpeg_escape_FF pad).  No masking: k_encode zero-fills every slot word
+//            past its chunk's last bit, and X / B are loaded only where they hold chunk bits.
+template <int R>
+__device__ __forceinline__ void group_values(const GroupWords &g, uint32_t kb, uint8_t *marks, int lane,
+                                             uint32_t (&v)[R]) {
+  const uint32_t span = 64u * R;
+  const uint32_t rsw = g.info & 0x1ffffu, wk = kb - g.k0;  // window start, relative to k0
+  const bool mk = lane >= 1 && lane < g.n && rsw >= wk && rsw < wk + span;
+  if (mk) marks[rsw - wk] = 1;
+  int base = __popcll(__ballot(lane >= 1 && lane < g.n && rsw < wk));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int own[R];
+  const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
 #pragma unroll
-  for (int j = 1; j < kChunksPerWave; j++) {
-    const uint32_t oj = __builtin_amdgcn_readlane(g.o_lane, j);
-    c += (j < g.n && k >= ((oj + 31) >> 5)) ? 1 : 0;
+  for (int i = 0; i < R; i++) {
+    const uint64_t m = __ballot(marks[64 * i + lane] != 0);
+    own[i] = base + __popcll(m & le);
+    base += __popcll(m);
   }
-  WordLoad r;
-  const uint32_t O = __shfl(g.o_lane, c, 64);
-  r.L = __shfl(g.l_lane, c, 64);
-  r.NL = __shfl(g.l_lane, c + 1, 64);
-  r.p = 32 * k - O;
-  r.has_next = g.c0 + c + 1 < g.nchunks;
-  const uint32_t *slot = g.slot0 + (size_t)c * kSlotWords;
-  const uint32_t wi = r.p >> 5;
-  r.w0 = slot[wi];
-  r.w1 = slot[min(wi + 1, (uint32_t)kSlotWords - 1)];  // clamped into the slot
-  r.w2 = slot[r.has_next ? kSlotWords : 0];            // next chunk's first word
-  return r;
-}
-
-__device__ __forceinline__ uint32_t word_value(const GroupWords &g, const WordLoad &r, uint32_t k) {
-  const uint32_t wi = r.p >> 5, s = r.p & 31, nw = (r.L + 31) >> 5;
-  const uint32_t w1 = wi + 1 < nw ? r.w1 : 0u;
-  uint32_t v = s ? (r.w0 << s) | (w1 >> (32 - s)) : r.w0;
-  const uint32_t rem = r.L - r.p;  // > 0: the word's first bit lies in its chunk
-  if (rem < 32) {
-    v &= ~(0xffffffffu >> rem);
-    if (r.has_next) v |= (r.NL < 32 ? r.w2 & ~(0xffffffffu >> r.NL) : r.w2) >> rem;
-  }
-  // The segment ends in this word: 1-bit padding to the byte boundary.  The word's owner
-  // need not be the last chunk: a short last chunk can start and end inside it.
-  const uint32_t endk = g.T - 32 * k;  // >= 1 (word k < k1)
-  if (endk < 32) {
-    const uint32_t pad = (8 - (g.T & 7)) & 7;
-    v |= (0xffffffffu >> endk) & ~(endk + pad >= 32 ? 0u : (0xffffffffu >> (endk + pad)));
-  }
-  return v;
-}
-
-__device__ __forceinline__ int ff_in_word(uint32_t v, uint32_t byte0, uint32_t total_bytes) {
-  int n = 0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (mk) marks[rsw - wk] = 0;
+  uint32_t A[R], B[R], X[R], inf[R];
+  bool bnd[R], own_nx[R];
 #pragma unroll
-  for (int b = 0; b < 4; b++)
-    n += (byte0 + b < total_bytes) && (((v >> (24 - 8 * b)) & 0xffu) == 0xffu);
-  return n;
+  for (int i = 0; i < R; i++) {
+    const uint32_t r = wk + 64u * i + (uint32_t)lane;  // word - k0
+    const bool valid = r < g.k1 - g.k0;  // lanes past k1: chunk 0's first word, no X / B loads
+    const int c = valid ? own[i] : 0;
+    inf[i] = bperm(g.info, c);
+    const uint32_t nsw = bperm(g.info, c + 1) & 0x1ffffu;
+    const uint32_t wi = valid ? r - (inf[i] & 0x1ffffu) : 0u;  // slot word under the first bit
+    const uint32_t off = (inf[i] >> 17) & 31u, rem = ((inf[i] >> 22) & 31u) + 1u;
+    bnd[i] = valid && r + 1 == nsw;  // chunk c's last owned word
+    own_nx[i] = valid && (lane == 63 || r + 1 == g.k1 - g.k0);  // lane + 1 does not hold word k + 1
+    const uint32_t *slot = g.slot0 + (size_t)(uint32_t)c * kSlotWords;
+    A[i] = slot[wi];
+    X[i] = (bnd[i] && off && rem > 32u - off) ? slot[wi + 1] : 0u;
+    const bool has_next = (inf[i] >> 27) & 1u;
+    B[i] = (own_nx[i] && (!bnd[i] || (rem < 32u && has_next))) ? slot[bnd[i] ? (uint32_t)kSlotWords : wi + 1] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    const uint32_t k = kb + 64u * i + (uint32_t)lane;
+    const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)A[i], 0x130, 0xf, 0xf, false);  // wave_shl:1
+    const uint32_t next = own_nx[i] ? B[i] : nx;
+    const uint32_t off = (inf[i] >> 17) & 31u, rem = ((inf[i] >> 22) & 31u) + 1u;
+    const uint32_t lo = off ? (bnd[i] ? X[i] : next) : A[i];
+    uint32_t w = __builtin_amdgcn_alignbit(A[i], lo, (32u - off) & 31u);
+    if (bnd[i] && rem < 32u) w |= next >> rem;  // the next chunk's first bits (0 past the segment)
+    const uint32_t endk = g.T - 32 * k;  // the segment ends in this word: 1-bit padding
+    if (endk < 32u) {
+      const uint32_t pad = (8u - (g.T & 7u)) & 7u;
+      w |= (0xffffffffu >> endk) & ~(endk + pad >= 32u ? 0u : (0xffffffffu >> (endk + pad)));
+    }
+    v[i] = w;
+  }
 }
 
+// 0xFF bytes of a word (exact per byte: no carries between bytes)
+__device__ __forceinline__ uint32_t ff_bytes(uint32_t v) {
+  const uint32_t y = ~v;
+  const uint32_t t = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);  // 0x80 per zero byte of y
+  return (uint32_t)__popc(t);
+}
+
+// agent-scope (all XCDs) store / load of the frame sizes k_scan_ff's last frame reads
+__device__ __forceinline__ void st_agent64(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t *p) {
+  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// frame header length: the default header, or (-huffman optimal) the default header without
+// its 348 table values plus the frame's own (k_huff_build's value counts)
+__device__ __forceinline__ uint32_t frame_hdr_len(int f, int hdr_len, const uint32_t *dht_nval) {
+  if (!dht_nval) return (uint32_t)hdr_len;
+  const uint32_t *nv = dht_nval + 4 * (size_t)f;
+  return (uint32_t)(hdr_len - 348) + nv[0] + nv[1] + nv[2] + nv[3];
+}
+
+// Wave per group: the group's words realigned into the segment's contiguous stream (word k of
+// segment s at stream[s * nchunks * kSlotWords + k], coalesced), and the 0xFF bytes among
+// them -> group_ff[gi].  (Bytes of the segment's last word past its padding are 0x00, so whole
+// words are counted.)
 __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ scratch,
                                                   const uint32_t *__restrict__ chunk_bits,
                                                   const uint32_t *__restrict__ chunk_off,
-                                                  const uint32_t *__restrict__ frame_bits,
-                                                  uint32_t *__restrict__ group_ff, int nchunks,
-                                                  int ngroups_per_frame, int ngroups) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+                                                  const uint32_t *__restrict__ seg_bits,
+                                                  uint32_t *__restrict__ group_ff, int nchunks, int gps,
+                                                  int ngroups, uint32_t *__restrict__ stream) {
+  __shared__ uint8_t s_marks[4][64 * kTailRounds];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gi = blockIdx.x * 4 + wave;
+  for (int i = lane; i < 64 * kTailRounds; i += 64) s_marks[wave][i] = 0;
   if (gi >= ngroups) return;
-  const GroupWords g =
-      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
-  int cnt = 0;
-  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
-    WordLoad ld[kWordsPerLane];
+  const GroupWords g = group_words(scratch, chunk_bits, chunk_off, seg_bits, nchunks, gps, gi, lane);
+  uint32_t *sw = stream + (size_t)g.s * nchunks * kSlotWords;  // the segment's realigned words
+  uint32_t cnt = 0;
+  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kTailRounds) {
+    uint32_t v[kTailRounds];
+    group_values<kTailRounds>(g, kb, s_marks[wave], lane, v);
 #pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
-    uint32_t v[kWordsPerLane];
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) {
+    for (int i = 0; i < kTailRounds; i++) {
       const uint32_t k = kb + 64 * i + lane;
-      if (k < g.k1) cnt += ff_in_word(v[i], 4 * k, g.total_bytes);
+      if (k < g.k1) {
+        cnt += ff_bytes(v[i]);
+        sw[k] = v[i];
+      }
     }
   }
-  cnt = wave_sum(cnt);
-  if (lane == 0) group_ff[gi] = (uint32_t)cnt;
+  cnt = (uint32_t)wave_sum((int)cnt);
+  if (lane == 0) group_ff[gi] = cnt;
 }
 
-// Per frame: exclusive scan of the chunk groups' 0xFF counts -> stuffed frame size.
-// -huffman optimal (dht_nval != null): the header length is per frame, hdr_base plus the
-// frame's table values, stored to hdr_lens for k_frame_hdr / k_write.
-__global__ __launch_bounds__(1024) void k_scan_ff(const uint32_t *__restrict__ group_ff,
-                                                  uint32_t *__restrict__ ff_off,
-                                                  const uint32_t *__restrict__ frame_bits,
-                                                  uint64_t *__restrict__ frame_size, int ngroups_per_frame,
-                                                  int hdr_len, const uint32_t *__restrict__ dht_nval,
-                                                  int hdr_base, uint32_t *__restrict__ hdr_lens) {
-  const int f = blockIdx.x;
-  const size_t g0 = (size_t)f * ngroups_per_frame;
-  const uint32_t t = block_excl_scan(group_ff + g0, ff_off + g0, ngroups_per_frame);
-  if (threadIdx.x == 0) {
-    uint32_t hl = (uint32_t)hdr_len;
-    if (dht_nval) {
-      hl = (uint32_t)hdr_base + dht_nval[4 * f] + dht_nval[4 * f + 1] + dht_nval[4 * f + 2] +
-           dht_nval[4 * f + 3];
-      hdr_lens[f] = hl;
+// Workgroup per frame: per segment (wave s % 4), the exclusive scan of its groups' 0xFF counts
+// (ff_off) and its stuffed size with the RSTn / EOI trailer; then the frame's size (header +
+// segments; RST: the segments' offsets after the header, seg_off).  The last frame to finish
+// (one ticket per frame, done[0], zeroed by k_scan_bits) places every frame: frame_offsets.
+__global__ __launch_bounds__(256) void k_scan_ff(const uint32_t *__restrict__ group_ff,
+                                                 uint32_t *__restrict__ ff_off,
+                                                 const uint32_t *__restrict__ seg_bits, int gps, int nseg,
+                                                 int hdr_len, const uint32_t *__restrict__ dht_nval,
+                                                 uint32_t *__restrict__ hdr_lens, uint32_t *__restrict__ seg_size,
+                                                 uint32_t *__restrict__ seg_off, uint64_t *__restrict__ frame_size,
+                                                 uint64_t *__restrict__ frame_offsets, uint32_t *__restrict__ done) {
+  __shared__ uint32_t s_last;
+  const int f = blockIdx.x, nframes = gridDim.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t mine = 0;  // nseg == 1: the segment's size (wave 0)
+  for (int si = wave; si < nseg; si += 4) {
+    const size_t s = (size_t)f * nseg + si, g0 = s * gps;
+    uint32_t carry = 0;
+    for (int i0 = 0; i0 < gps; i0 += 64) {
+      const int i = i0 + lane;
+      const uint32_t v = i < gps ? group_ff[g0 + i] : 0u;
+      const uint32_t incl = wave_incl_scan(v, lane);
+      if (i < gps) ff_off[g0 + i] = carry + incl - v;
+      carry += lane63(incl);
     }
-    frame_size[f] = (uint64_t)hl + ((frame_bits[f] + 7) >> 3) + t + 2;
+    mine = ((seg_bits[s] + 7) >> 3) + carry + 2;
+    if (nseg > 1 && lane == 0) seg_size[s] = mine;
   }
-}
-
-// RST mode, per segment (wave): scan of its groups' 0xFF counts -> stuffed segment size
-// including the 2-byte trailer (RSTn or, for the frame's last segment, EOI).
-__global__ __launch_bounds__(256) void k_scan_ff_seg(const uint32_t *__restrict__ group_ff,
-                                                     uint32_t *__restrict__ ff_off,
-                                                     const uint32_t *__restrict__ seg_bits,
-                                                     uint64_t *__restrict__ seg_size, int ngroups_per_seg,
-                                                     int nsegs) {
-  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (sg >= nsegs) return;
-  const size_t g0 = (size_t)sg * ngroups_per_seg;
-  const uint32_t t = wave_excl_scan_arr(group_ff + g0, ff_off + g0, ngroups_per_seg, lane);
-  if (lane == 0) seg_size[sg] = (uint64_t)((seg_bits[sg] + 7) >> 3) + t + 2;
-}
-
-// RST mode (one entropy-coded segment per MCU row): per frame, the segments' offsets after
-// the header (exclusive scan of their stuffed sizes, each including its 2-byte trailer:
-// RSTn, or EOI for the last) and the frame size = header + all segments.
-__global__ __launch_bounds__(64) void k_seg_sizes(const uint64_t *__restrict__ seg_size, int nseg,
-                                                  int hdr_len, uint32_t *__restrict__ seg_off,
-                                                  uint64_t *__restrict__ frame_size) {
-  const int f = blockIdx.x, lane = threadIdx.x;
-  uint32_t carry = 0;
-  for (int s0 = 0; s0 < nseg; s0 += 64) {
-    const int s = s0 + lane;
-    const uint32_t v = s < nseg ? (uint32_t)seg_size[(size_t)f * nseg + s] : 0u;
-    const uint32_t incl = wave_incl_scan(v, lane);
-    if (s < nseg) seg_off[(size_t)f * nseg + s] = carry + incl - v;
-    carry += lane63(incl);
+  __syncthreads();  // seg_size of the frame written (RST)
+  const uint32_t hl = frame_hdr_len(f, hdr_len, dht_nval);
+  if (wave == 0) {
+    uint64_t fsz = hl;
+    if (nseg == 1) {
+      fsz += mine;
+    } else {
+      uint32_t carry = 0;
+      for (int i0 = 0; i0 < nseg; i0 += 64) {
+        const int i = i0 + lane;
+        const uint32_t v = i < nseg ? seg_size[(size_t)f * nseg + i] : 0u;
+        const uint32_t incl = wave_incl_scan(v, lane);
+        if (i < nseg) seg_off[(size_t)f * nseg + i] = carry + incl - v;
+        carry += lane63(incl);
+      }
+      fsz += carry;
+    }
+    if (lane == 0) {
+      if (dht_nval) hdr_lens[f] = hl;
+      st_agent64(frame_size + f, fsz);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(done, 1u);
+    if (lane == 0) s_last = t;
   }
-  if (lane == 0) frame_size[f] = (uint64_t)hdr_len + carry;
-}
-
-// One wave per frame: packed output offset (sum of the preceding frame sizes), capacity
-// check, header (SOI .. SOS) and EOI of the frame; in RST mode (seg_off != null) also the
-// RST0..7 marker closing every segment but the last (mjpegenc.c ff_mjpeg_encode_stuffing:
-// RST0 + (mb_y & 7) after MCU row mb_y).  -huffman optimal (hdr_lens != null):
-// the default header's bytes before and after its DHT around the frame's own DHT
-// (jpeg_table_header: one DHT, tables DC0, DC1, AC0, AC1).
-__global__ __launch_bounds__(64) void k_frame_hdr(const uint64_t *__restrict__ frame_size,
-                                                  const uint8_t *__restrict__ hdr, int hdr_len,
-                                                  uint8_t *__restrict__ out, uint64_t out_cap,
-                                                  uint64_t *__restrict__ frame_offsets,
-                                                  uint32_t *__restrict__ status,
-                                                  const uint32_t *__restrict__ hdr_lens, int dht_pos,
-                                                  int dht_end, const uint8_t *__restrict__ dht,
-                                                  const uint32_t *__restrict__ dht_nval,
-                                                  const uint32_t *__restrict__ seg_off,
-                                                  const uint64_t *__restrict__ seg_size, int nseg) {
-  const int f = blockIdx.x, lane = threadIdx.x;
-  uint64_t s = 0;
-  for (int i = lane; i < f; i += 64) s += frame_size[i];
+  __syncthreads();
+  if (s_last != (uint32_t)nframes - 1 || wave != 0) return;
+  // the last frame: packed offsets of every frame
+  uint64_t carry = 0;
+  for (int i0 = 0; i0 < nframes; i0 += 64) {
+    const int i = i0 + lane;
+    const uint64_t v = i < nframes ? ld_agent64(frame_size + i) : 0ull;
+    uint64_t incl = v;
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
-  const uint64_t fsize = frame_size[f];
-  if (lane == 0) {
-    frame_offsets[f] = s;
-    if (f == (int)gridDim.x - 1) frame_offsets[f + 1] = s + fsize;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    if (i < nframes) frame_offsets[i] = carry + incl - v;
+    carry += __shfl(incl, 63, 64);
   }
-  if (s + fsize > out_cap) {
+  if (lane == 0) frame_offsets[nframes] = carry;
+}
+
+// The frame header at fo (hl bytes): the default header, or (-huffman optimal) its bytes
+// before and after the DHT around the frame's own DHT (jpeg_table_header: one DHT, tables
+// DC0, DC1, AC0, AC1).
+__device__ __noinline__ void write_header(uint8_t *fo, int f, const uint8_t *hdr, int hdr_len, int dht_pos,
+                                             int dht_end, const uint8_t *dht, const uint32_t *dht_nval, int lane) {
+  if (!dht_nval) {
+    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
+    return;
+  }
+  const uint32_t *nv = dht_nval + 4 * (size_t)f;
+  const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
+  for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
+  uint8_t *o = fo + dht_pos;
+  if (lane == 0) {
+    o[0] = 0xff;
+    o[1] = 0xc4;
+    o[2] = (uint8_t)(len >> 8);
+    o[3] = (uint8_t)len;
+  }
+  o += 4;
+  for (int t = 0; t < 4; t++) {
+    const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
+    const int n = 16 + (int)nv[t];
+    if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
+    for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
+    o += 1 + n;
+  }
+  const int tail = hdr_len - dht_end;
+  for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
+}
+
+typedef uint32_t u32_any __attribute__((aligned(1)));  // a dword at any byte address (global memory)
+
+// nb bytes of a word, MSB first, each 0xFF followed by 0x00
+__device__ __noinline__ void write_stuffed(uint8_t *p, uint32_t w, uint32_t nb) {
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint8_t byte = (uint8_t)(w >> (24 - 8 * b));
+    *p++ = byte;
+    if (byte == 0xff) *p++ = 0;
+  }
+}
+
+// Wave per chunk group: the group's words from the stream k_count_ff realigned, with a 0x00
+// after every 0xFF (ff_mjpeg_escape_FF), at frame offset + header + segment offset + 4 k + the
+// 0xFFs before word k in the segment.  A word without 0xFF goes out as one unaligned dword
+// store (byte-swapped: the scan is MSB first), a word with 0xFF bytes as byte stores.
+__global__ __launch_bounds__(256) void k_write(
+    const uint32_t *__restrict__ stream, const uint32_t *__restrict__ chunk_bits,
+    const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ seg_bits,
+    const uint32_t *__restrict__ ff_off, int nchunks, int gps, int nseg, int nframes,
+    const uint32_t *__restrict__ seg_size, const uint32_t *__restrict__ seg_off,
+    const uint64_t *__restrict__ frame_offsets, const uint8_t *__restrict__ hdr, int hdr_len,
+    const uint32_t *__restrict__ hdr_lens, int dht_pos, int dht_end, const uint8_t *__restrict__ dht,
+    const uint32_t *__restrict__ dht_nval, uint8_t *__restrict__ out, uint64_t out_cap,
+    uint32_t *__restrict__ status) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gi = blockIdx.x * 4 + wave, ngroups = gps * nseg * nframes;
+  if (gi >= ngroups) return;
+  const int s = gi / gps, gx = gi - s * gps, f = s / nseg, si = s - f * nseg;
+  const int c0 = gx * kChunksPerWave, cl = min(c0 + kChunksPerWave, nchunks) - 1;
+  const size_t i0 = (size_t)s * nchunks;
+  const uint32_t k0 = (chunk_off[i0 + c0] + 31) >> 5, k1 = (chunk_off[i0 + cl] + chunk_bits[i0 + cl] + 31) >> 5;
+  const uint32_t total_bytes = (seg_bits[s] + 7) >> 3;
+  const uint64_t foff = frame_offsets[f];
+  if (frame_offsets[f + 1] > out_cap) {  // the host regrows the output and runs k_write again
     if (lane == 0) atomicOr(status, 1u);
     return;
   }
-  uint8_t *fo = out + s;
-  if (!hdr_lens) {
-    for (int i = lane; i < hdr_len; i += 64) fo[i] = hdr[i];
-  } else {
-    const uint32_t *nv = dht_nval + 4 * (size_t)f;
-    const int len = 2 + 4 * 17 + (int)(nv[0] + nv[1] + nv[2] + nv[3]);
-    for (int i = lane; i < dht_pos; i += 64) fo[i] = hdr[i];
-    uint8_t *o = fo + dht_pos;
-    if (lane == 0) {
-      o[0] = 0xff;
-      o[1] = 0xc4;
-      o[2] = (uint8_t)(len >> 8);
-      o[3] = (uint8_t)len;
-    }
-    o += 4;
-    for (int t = 0; t < 4; t++) {
-      const uint8_t *src = dht + ((size_t)f * 4 + t) * kDhtSlot;
-      const int n = 16 + (int)nv[t];
-      if (lane == 0) o[0] = (uint8_t)(t < 2 ? t : 0x10 | (t - 2));
-      for (int i = lane; i < n; i += 64) o[1 + i] = src[i];
-      o += 1 + n;
-    }
-    const int tail = hdr_len - dht_end;
-    for (int i = lane; i < tail; i += 64) o[i] = hdr[dht_end + i];
+  const uint32_t hl = hdr_lens ? hdr_lens[f] : (uint32_t)hdr_len;
+  const uint64_t sbase = foff + hl + (nseg > 1 ? seg_off[s] : 0u);
+  if (si == 0 && gx == 0) write_header(out + foff, f, hdr, hdr_len, dht_pos, dht_end, dht, dht_nval, lane);
+  if (gx == gps - 1 && lane == 0) {  // the segment's trailer: RSTn, or EOI after the frame's last
+    const uint64_t segsz = nseg > 1 ? seg_size[s] : frame_offsets[f + 1] - foff - hl;
+    uint8_t *m = out + sbase + segsz - 2;
+    m[0] = 0xff;
+    m[1] = si == nseg - 1 ? 0xd9 : (uint8_t)(0xd0 + (si & 7));
   }
-  if (lane == 0) {
-    fo[fsize - 2] = 0xff;
-    fo[fsize - 1] = 0xd9;
-  }
-  if (seg_off)
-    for (int sg = lane; sg < nseg - 1; sg += 64) {
-      const size_t i = (size_t)f * nseg + sg;
-      uint8_t *m = fo + hdr_len + seg_off[i] + seg_size[i] - 2;
-      m[0] = 0xff;
-      m[1] = (uint8_t)(0xd0 + (sg & 7));
-    }
-}
-
-// Wave per chunk group, lanes = words: the group's owned bytes with a 0x00 after every
-// 0xFF (ff_mjpeg_escape_FF) at header + unstuffed position + the 0xFFs before it in the
-// frame (group prefix from k_scan_ff, in-group prefix by a wave scan).
-__global__ __launch_bounds__(256) void k_write(
-    const uint32_t *__restrict__ scratch, const uint32_t *__restrict__ chunk_bits,
-    const uint32_t *__restrict__ chunk_off, const uint32_t *__restrict__ frame_bits,
-    const uint32_t *__restrict__ ff_off, const uint64_t *__restrict__ frame_size,
-    const uint64_t *__restrict__ frame_offsets, int hdr_len, const uint32_t *__restrict__ hdr_lens,
-    int nchunks, int ngroups_per_frame, int ngroups, uint8_t *__restrict__ out, uint64_t out_cap,
-    const uint32_t *__restrict__ seg_off, int nseg) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (gi >= ngroups) return;
-  // g.f is the entropy-coded segment (the frame itself unless RST mode)
-  const GroupWords g =
-      group_words(scratch, chunk_bits, chunk_off, frame_bits, nchunks, ngroups_per_frame, gi, lane);
-  const int fr = g.f / nseg;
-  const uint64_t foff = frame_offsets[fr];
-  if (foff + frame_size[fr] > out_cap) return;  // k_frame_hdr flagged the overflow
-  const uint32_t hl = hdr_lens ? hdr_lens[fr] : (uint32_t)hdr_len;
-  uint8_t *base = out + foff + hl + (seg_off ? seg_off[g.f] : 0u) + 4 * (size_t)g.k0 + ff_off[gi];
+  const uint32_t *sw = stream + i0 * kSlotWords;
+  uint8_t *ob = out + sbase + ff_off[gi];  // + 4 k + the word's 0xFF prefix in the group
   uint32_t carry = 0;
-  for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kWordsPerLane) {
-    WordLoad ld[kWordsPerLane];
+  for (uint32_t kb = k0; kb < k1; kb += 64 * kTailRounds) {
+    uint32_t v[kTailRounds];
 #pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) ld[i] = word_load(g, min(kb + 64 * i + lane, g.k1 - 1));
-    uint32_t v[kWordsPerLane], cnt[kWordsPerLane];
+    for (int i = 0; i < kTailRounds; i++) v[i] = sw[min(kb + 64 * i + lane, k1 - 1)];
 #pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) v[i] = word_value(g, ld[i], min(kb + 64 * i + lane, g.k1 - 1));
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) {
+    for (int i = 0; i < kTailRounds; i++) {
+      if (kb + 64 * i >= k1) break;  // wave-uniform
       const uint32_t k = kb + 64 * i + lane;
-      cnt[i] = k < g.k1 ? (uint32_t)ff_in_word(v[i], 4 * k, g.total_bytes) : 0u;
-    }
-#pragma unroll
-    for (int i = 0; i < kWordsPerLane; i++) {
-      const uint32_t k = kb + 64 * i + lane;
-      const uint32_t incl = wave_incl_scan(cnt[i], lane);
-      if (k < g.k1) {
-        uint8_t *p = base + 4 * (k - g.k0) + carry + incl - cnt[i];
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-          if (4 * k + bb < g.total_bytes) {
-            const uint8_t byte = (uint8_t)(v[i] >> (24 - 8 * bb));
-            *p++ = byte;
-            if (byte == 0xff) *p++ = 0;
-          }
-        }
+      const bool valid = k < k1;
+      const uint32_t w = v[i];
+      const uint32_t ff = valid ? ff_bytes(w) : 0u;
+      const uint32_t incl = wave_incl_scan(ff, lane);
+      uint8_t *p = ob + 4 * (size_t)k + carry + incl - ff;
+      const bool last = valid && 4 * k + 4 > total_bytes;  // the segment's last word: nb < 4 bytes
+      if (valid && ff == 0 && !last) {
+        *(u32_any *)p = __builtin_bswap32(w);
+      } else if (valid) {
+        write_stuffed(p, w, min(4u, total_bytes - 4 * k));
       }
       carry += lane63(incl);
     }
