@@ -1763,11 +1763,26 @@ __device__ __forceinline__ void group_values(const GroupWords &g, uint32_t kb, u
     const uint32_t off = (inf[i] >> 17) & 31u, rem = ((inf[i] >> 22) & 31u) + 1u;
     bnd[i] = valid && r + 1 == nsw;  // chunk c's last owned word
     own_nx[i] = valid && (lane == 63 || r + 1 == g.k1 - g.k0);  // lane + 1 does not hold word k + 1
+#ifdef MJG_EXP_BRANCHFREE
+    // 32-bit byte offsets from the group's first slot; X / B load A's word when not needed
+    const uint8_t *s0 = (const uint8_t *)g.slot0;
+    const uint32_t oa = __umul24((uint32_t)c, kSlotWords * 4u) + (wi << 2);
+    const bool nX = bnd[i] && off && rem > 32u - off;
+    const bool has_next = (inf[i] >> 27) & 1u;
+    const bool nB = own_nx[i] && (!bnd[i] || (rem < 32u && has_next));
+    const uint32_t ob = bnd[i] ? __umul24((uint32_t)c + 1u, kSlotWords * 4u) : oa + 4u;
+    A[i] = *(const uint32_t *)(s0 + oa);
+    X[i] = *(const uint32_t *)(s0 + (nX ? oa + 4u : oa));
+    B[i] = *(const uint32_t *)(s0 + (nB ? ob : oa));
+    X[i] = nX ? X[i] : 0u;
+    B[i] = nB ? B[i] : 0u;
+#else
     const uint32_t *slot = g.slot0 + (size_t)(uint32_t)c * kSlotWords;
     A[i] = slot[wi];
     X[i] = (bnd[i] && off && rem > 32u - off) ? slot[wi + 1] : 0u;
     const bool has_next = (inf[i] >> 27) & 1u;
     B[i] = (own_nx[i] && (!bnd[i] || (rem < 32u && has_next))) ? slot[bnd[i] ? (uint32_t)kSlotWords : wi + 1] : 0u;
+#endif
   }
 #pragma unroll
   for (int i = 0; i < R; i++) {
@@ -1836,7 +1851,9 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
       const uint32_t k = kb + 64 * i + lane;
       if (k < g.k1) {
         cnt += ff_bytes(v[i]);
+#ifndef MJG_EXP_COUNT_NOSTREAM
         sw[k] = v[i];
+#endif
       }
     }
   }
@@ -1949,15 +1966,6 @@ __device__ __noinline__ void write_header(uint8_t *fo, int f, const uint8_t *hdr
 
 typedef uint32_t u32_any __attribute__((aligned(1)));  // a dword at any byte address (global memory)
 
-// nb bytes of a word, MSB first, each 0xFF followed by 0x00
-__device__ __noinline__ void write_stuffed(uint8_t *p, uint32_t w, uint32_t nb) {
-  for (uint32_t b = 0; b < nb; b++) {
-    const uint8_t byte = (uint8_t)(w >> (24 - 8 * b));
-    *p++ = byte;
-    if (byte == 0xff) *p++ = 0;
-  }
-}
-
 // Wave per chunk group: the group's words from the stream k_count_ff realigned, with a 0x00
 // after every 0xFF (ff_mjpeg_escape_FF), at frame offset + header + segment offset + 4 k + the
 // 0xFFs before word k in the segment.  A word without 0xFF goes out as one unaligned dword
@@ -2010,10 +2018,31 @@ __global__ __launch_bounds__(256) void k_write(
       const uint32_t incl = wave_incl_scan(ff, lane);
       uint8_t *p = ob + 4 * (size_t)k + carry + incl - ff;
       const bool last = valid && 4 * k + 4 > total_bytes;  // the segment's last word: nb < 4 bytes
+#ifdef MJG_EXP_WRITE_NOSTORE
+      if (w == 0x12345678u && k == 7u) *(u32_any *)p = 0u;  // keeps the loads alive
+      else
+#endif
       if (valid && ff == 0 && !last) {
+#ifndef MJG_EXP_WRITE_NOSTORE
         *(u32_any *)p = __builtin_bswap32(w);
-      } else if (valid) {
-        write_stuffed(p, w, min(4u, total_bytes - 4 * k));
+#endif
+      } else if (valid) {  // 0xFF bytes (each then 0x00), or the segment's last (short) word
+        const uint32_t nb = min(4u, total_bytes - 4 * k);
+        uint64_t X = 0;
+        uint32_t len = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t byte = (w >> (24 - 8 * b)) & 0xffu;
+          if ((uint32_t)b < nb) {
+            X |= (uint64_t)byte << (8 * len);
+            len += byte == 0xffu ? 2u : 1u;
+          }
+        }
+        const uint32_t first = len >= 4u ? 4u : 0u;
+        if (len >= 4u) *(u32_any *)p = (uint32_t)X;
+#pragma unroll
+        for (uint32_t b = 0; b < 8; b++)
+          if (b >= first && b < len) p[b] = (uint8_t)(X >> (8 * b));
       }
       carry += lane63(incl);
     }
