@@ -173,6 +173,10 @@ struct PlaneScale {
 // its previous submit (mjg_sync waits for `done`), so no device-side wait guards it.
 struct Slot {
   bool alloc = false, pending = false;
+  hipStream_t st = nullptr;        // H2D, scale and k_encode of this slot's submits
+  uint8_t *d_stage = nullptr;      // H2D staging for host submits (allocated on first use)
+  uint8_t *d_scaled = nullptr;     // -vf scale: k_scale's output planes
+  uint32_t *d_stage_bits = nullptr;  // k_encode: per wave, lane-major staging of blocks past 128 bits
   int n = 0;
   uint64_t total = 0;
   uint32_t *d_scratch = nullptr;
@@ -201,7 +205,9 @@ struct Slot {
 struct mjg_ctx {
   int device = 0;
   mjg_config cfg{};
-  hipStream_t stream = nullptr;  // H2D, scale, k_encode
+  hipStream_t stream = nullptr;  // H2D, scale, k_encode of slot 0's submits
+  hipStream_t stream2 = nullptr; // ... of slot 1's: consecutive submits' k_encode launches overlap
+                                 // (the next one starts on the CUs the previous one's drain frees)
   hipStream_t tail = nullptr;    // scans, stuffing, write, D2H of the sizes
   EncGeom geom{};
   int32_t qmat[64];
@@ -213,8 +219,7 @@ struct mjg_ctx {
 
   uint32_t *d_tabs = nullptr;
   uint8_t *d_hdr = nullptr;
-  uint8_t *d_stage = nullptr, *d_scaled = nullptr;
-  uint32_t *d_stage_bits = nullptr;  // k_encode: per wave, lane-major staging of blocks past 128 bits
+  size_t stage_cols = 0;       // staging columns per slot (persistent waves of k_encode / k_emit_syms / fused)
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
@@ -244,15 +249,16 @@ void free_ctx(mjg_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   if (c->tail) (void)hipStreamSynchronize(c->tail);
-  void *ptrs[] = {c->d_tabs, c->d_hdr, c->d_stage, c->d_scaled, c->d_stage_bits, c->ps[0].hcp,
+  void *ptrs[] = {c->d_tabs, c->d_hdr, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
                   c->ps[0].hsum, c->ps[1].hsum, c->ps[1].vps, c->ps[0].d_fh, c->ps[0].d_fv,
                   c->ps[1].d_fh, c->ps[1].d_fv};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
-    void *sp[] = {S.d_scratch, S.d_stream, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
+    void *sp[] = {S.d_stage, S.d_scaled, S.d_stage_bits, S.d_scratch, S.d_stream, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
                   S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_done, S.d_out,
                   S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg, S.d_syms, S.d_symn};
     for (void *p : sp)
@@ -268,6 +274,7 @@ void free_ctx(mjg_ctx *c) {
   }
   if (c->h_fetch) (void)hipHostFree(c->h_fetch);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->tail) (void)hipStreamDestroy(c->tail);
   delete c;
 }
@@ -396,6 +403,15 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   const size_t B = c->slot_B, NC = c->slot_NC, NS = c->slot_NS;
   const EncGeom &g = c->geom;
   int rc;
+  // Slot 1 on its own stream where a submit is a chain of launches that each drain the GPU
+  // (-huffman optimal: count pass, table build, emission; -vf scale: k_scale, k_encode): the
+  // next submit's chain then starts on the CUs the previous one's drains free (A/B: c1 +24%,
+  // c4 +1.7%).  A plain default-table submit is one k_encode launch: overlapping consecutive
+  // launches measured +1.1% (c2) while each launch's own time grew 5%, so those stay on one
+  // stream (launches back to back, per-launch times comparable).
+  S.st = (&S == &c->slot[1] && (c->optimal || c->scale)) ? c->stream2 : c->stream;
+  if ((rc = dmalloc(&S.d_stage_bits, c->stage_cols * 64 * kStageWords))) return rc;
+  if (c->scale && !c->fused && (rc = dmalloc(&S.d_scaled, B * c->enc_frame_bytes))) return rc;
   if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&S.d_stream, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&S.d_chunk_bits, B * NC)) || (rc = dmalloc(&S.d_chunk_off, B * NC)) ||
@@ -541,6 +557,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   if (device < 0 || device >= ndev) return set_err(MJG_E_INVALID, "device %d of %d", device, ndev);
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));
 
   c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
@@ -693,7 +710,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->slot_NS = NS;
   c->timing = (k.flags & (MJG_F_TIMING | MJG_F_TIMING_DETAIL)) != 0;
   c->timing_detail = (k.flags & MJG_F_TIMING_DETAIL) != 0;
-  if ((rc = alloc_slot(c, c->slot[0]))) return rc;
   HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
 
@@ -754,8 +770,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
         HIP_TRY(hipMemcpy(ps.d_fh, ps.fh.data(), ps.fh.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(ps.d_fv, ps.fv.data(), ps.fv.size() * 4, hipMemcpyHostToDevice));
       }
-    } else if ((rc = dmalloc(&c->d_scaled, B * c->enc_frame_bytes))) {
-      return rc;
     }
   }
 
@@ -775,12 +789,8 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     c->fused_grid = std::max(1, ncu * std::max(1, fper));
     stage_cols = std::max(stage_cols, (size_t)c->fused_grid * kFusedWaves);
   }
-  {
-    const int rc2 = dmalloc(&c->d_stage_bits, stage_cols * 64 * kStageWords);
-    if (rc2) return rc2;
-  }
-
-  return MJG_OK;
+  c->stage_cols = stage_cols;
+  return alloc_slot(c, c->slot[0]);
 }
 
 // HIP events: with MJG_F_TIMING around scale, huff, encode and the whole tail (scan .. write,
@@ -790,7 +800,7 @@ void tmark(mjg_ctx *c, Slot &S, int k, int end) {
   if (!c->timing) return;
   const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
   if (tail && !c->timing_detail) return;
-  (void)hipEventRecord(S.ev[k][end], tail ? c->tail : c->stream);
+  (void)hipEventRecord(S.ev[k][end], tail ? c->tail : S.st);
 }
 
 // status: reset the overflow flag first (the regrow path; a submit's scan kernel resets it)
@@ -816,10 +826,10 @@ int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
 
 template <int HT, int NPV, bool RANGE_ON, int MODE>
 void launch_fused3(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
-  k_scale_encode<HT, NPV, RANGE_ON, MODE><<<c->fused_grid, 64 * kFusedWaves, 0, c->stream>>>(
+  k_scale_encode<HT, NPV, RANGE_ON, MODE><<<c->fused_grid, 64 * kFusedWaves, 0, S.st>>>(
       src, c->geom, c->fgeom, c->d_tabs, (const uint32_t *)c->ps[0].d_fh, (const uint32_t *)c->ps[0].d_fv,
       (const uint32_t *)c->ps[1].d_fh, (const uint32_t *)c->ps[1].d_fv, S.d_scratch, S.d_chunk_bits,
-      c->d_stage_bits, S.d_work, n, S.d_hist, S.d_syms, S.d_symn);
+      S.d_stage_bits, S.d_work, n, S.d_hist, S.d_syms, S.d_symn);
 }
 
 template <int MODE>
@@ -835,13 +845,13 @@ template <int MODE, bool MF>
 void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
   if (g.range_convert)
-    k_encode<true, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
+    k_encode<true, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        c->d_stage_bits, S.d_syms, S.d_symn);
+        S.d_stage_bits, S.d_syms, S.d_symn);
   else
-    k_encode<false, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, c->stream>>>(
+    k_encode<false, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
-        c->d_stage_bits, S.d_syms, S.d_symn);
+        S.d_stage_bits, S.d_syms, S.d_symn);
 }
 
 // The DCT stage: the VALU passes, or (-huffman default) dct_mfma.
@@ -923,13 +933,12 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   }
   const uint8_t *src = frames;
   if (!src_is_device) {
-    if (!c->d_stage) {  // staging for host submits, allocated on first use
-      const int rc = dmalloc(&c->d_stage, (size_t)c->cfg.max_batch * c->in_frame_bytes);
+    if (!S.d_stage) {  // staging for host submits, allocated on first use
+      const int rc = dmalloc(&S.d_stage, (size_t)c->cfg.max_batch * c->in_frame_bytes);
       if (rc) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(c->d_stage, frames, (size_t)n * c->in_frame_bytes, hipMemcpyHostToDevice,
-                           c->stream));
-    src = c->d_stage;
+    HIP_TRY(hipMemcpyAsync(S.d_stage, frames, (size_t)n * c->in_frame_bytes, hipMemcpyHostToDevice, S.st));
+    src = S.d_stage;
   }
   const uint8_t *enc_in = src;
   if (c->scale && !c->fused) {
@@ -956,13 +965,13 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
 #define MJG_SCALE_LAUNCH3(HT, NPV, D4, TH)                                                          \
   do {                                                                                              \
     if (sg.range == 1)                                                                              \
-      k_scale<HT, NPV, D4, 1, TH><<<grid, 64 * scale_waves(TH), ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+      k_scale<HT, NPV, D4, 1, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(src, S.d_scaled, sg, ps.hcp,        \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
     else if (sg.range == 2)                                                                         \
-      k_scale<HT, NPV, D4, 2, TH><<<grid, 64 * scale_waves(TH), ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+      k_scale<HT, NPV, D4, 2, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(src, S.d_scaled, sg, ps.hcp,        \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
     else                                                                                            \
-      k_scale<HT, NPV, D4, 0, TH><<<grid, 64 * scale_waves(TH), ps.lds, c->stream>>>(src, c->d_scaled, sg, ps.hcp,    \
+      k_scale<HT, NPV, D4, 0, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(src, S.d_scaled, sg, ps.hcp,        \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
   } while (0)
 #define MJG_SCALE_LAUNCH(HT, NPV, TH)      \
@@ -987,27 +996,27 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     }
     tmark(c, S, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());
-    enc_in = c->d_scaled;
+    enc_in = S.d_scaled;
   }
   const int ntasks = g.nchunks * g.nseg * n;
   const int nsegs = g.nseg * n;  // entropy-coded segments of this submit
   const int wgs = std::min((ntasks + kWavesPerWg - 1) / kWavesPerWg, c->enc_grid);
   if (c->optimal) {  // pass 1: symbol counts per frame, then the frame's tables
     tmark(c, S, MJG_K_HUFF, 0);
-    HIP_TRY(hipMemsetAsync(S.d_hist, 0, (size_t)n * kFrameTabWords * 4, c->stream));
+    HIP_TRY(hipMemsetAsync(S.d_hist, 0, (size_t)n * kFrameTabWords * 4, S.st));
     if (c->fused)
       launch_fused<kCount>(c, S, src, n);
     else
       launch_encode<kCount>(c, S, enc_in, wgs, ntasks);
-    HIP_TRY(hipMemsetAsync(S.d_work, 0, (size_t)kXcds * kCtrStride * 4, c->stream));  // unit counters for pass 2
-    k_huff_build<<<n * 4, 64, 0, c->stream>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
+    HIP_TRY(hipMemsetAsync(S.d_work, 0, (size_t)kXcds * kCtrStride * 4, S.st));  // unit counters for pass 2
+    k_huff_build<<<n * 4, 64, 0, S.st>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
     tmark(c, S, MJG_K_HUFF, 1);
     HIP_TRY(hipGetLastError());
   }
   tmark(c, S, MJG_K_ENCODE, 0);
   if (c->optimal)
-    k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, c->stream>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
-                                                                  S.d_scratch, S.d_chunk_bits, c->d_stage_bits,
+    k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, S.st>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
+                                                             S.d_scratch, S.d_chunk_bits, S.d_stage_bits,
                                                                   ntasks);
   else if (c->fused)
     launch_fused<kEmitDefault>(c, S, src, n);
@@ -1015,7 +1024,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     launch_encode<kEmitDefault>(c, S, enc_in, wgs, ntasks);
   tmark(c, S, MJG_K_ENCODE, 1);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(S.enc_done, c->stream));
+  HIP_TRY(hipEventRecord(S.enc_done, S.st));
   HIP_TRY(hipStreamWaitEvent(c->tail, S.enc_done, 0));
   if (c->timing && !c->timing_detail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->tail);
   tmark(c, S, MJG_K_SCAN_BITS, 0);
@@ -1156,7 +1165,7 @@ int mjg_output_device(mjg_ctx *c, const uint8_t **data, const uint64_t **offsets
   return MJG_OK;
 }
 
-void *mjg_stream(mjg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+void *mjg_stream(mjg_ctx *c) { return c ? (void *)(c->slot[c->head].st ? c->slot[c->head].st : c->stream) : nullptr; }
 
 int mjg_host_alloc(size_t bytes, void **ptr) {
   if (!ptr) return set_err(MJG_E_INVALID, "null argument");
@@ -1242,15 +1251,16 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
 
 int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  if (!c->d_scaled) return set_err(MJG_E_STATE, "context does not scale, or scales fused (opened with MJG_F_FUSED)");
-  if (c->nout > 0) {  // the scaled planes are shared by the slots: only the latest submit's
+  if (!c->scale || c->fused)
+    return set_err(MJG_E_STATE, "context does not scale, or scales fused (opened with MJG_F_FUSED)");
+  if (c->nout > 0) {  // the latest synced submit's planes
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;
   }
   if (c->nout > 0 || c->last < 0) return set_err(MJG_E_STATE, "sync every queued submit first");
   if (frame < 0 || frame >= c->slot[c->last].n) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (cap < c->enc_frame_bytes) return set_err(MJG_E_CAPACITY, "need %zu bytes", c->enc_frame_bytes);
-  HIP_TRY(hipMemcpy(out, c->d_scaled + (size_t)frame * c->enc_frame_bytes, c->enc_frame_bytes,
+  HIP_TRY(hipMemcpy(out, c->slot[c->last].d_scaled + (size_t)frame * c->enc_frame_bytes, c->enc_frame_bytes,
                     hipMemcpyDeviceToHost));
   return MJG_OK;
 }

@@ -79,8 +79,8 @@ extern "C" {
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */
 #define MJG_K_ENCODE 1         /* load [+ fused scale] + FDCT + quant + Huffman -> chunk bits */
 #define MJG_K_SCAN_BITS 2      /* per-frame exclusive scan of chunk bit lengths      */
-#define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk      */
-#define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes        */
+#define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk group */
+#define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes, offsets */
 #define MJG_K_WRITE 5          /* header + stuffed scan + EOI into packed output     */
 #define MJG_K_HUFF 6           /* -huffman optimal: symbol-count pass + table build   */
 #define MJG_K_TAIL 7           /* MJG_K_SCAN_BITS .. MJG_K_WRITE as one interval (MJG_F_TIMING) */
@@ -138,7 +138,9 @@ int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_devi
  * exceeded its capacity. */
 int mjg_sync(mjg_ctx *ctx, uint64_t *frame_sizes, uint64_t *total);
 /* Copy the packed JPEGs of the last synced submit (frame after frame) to host memory; syncs
- * the oldest queued submit first when mjg_sync was not called since the last mjg_submit. */
+ * the oldest queued submit first when mjg_sync was not called since the last mjg_submit.
+ * The bytes go through the context's page-locked buffer (mjg_fetch_host) and are then copied
+ * into `out`: one host copy more than mjg_fetch_host, which avoids it. */
 int mjg_fetch(mjg_ctx *ctx, uint8_t *out, size_t cap);
 /* The same bytes without the copy into caller memory: *data points at the context's
  * page-locked copy (DMA'd from the device), *len its size; valid until the next
@@ -147,8 +149,9 @@ int mjg_fetch_host(mjg_ctx *ctx, const uint8_t **data, size_t *len);
 /* Device pointers of the packed output and of the per-frame byte offsets (nframes+1
  * entries, valid after mjg_sync). */
 int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offsets);
-/* The hipStream_t the context launches H2D, scale and k_encode on (for event timing by the
- * caller; the tail kernels run on a second stream ordered after k_encode). */
+/* The hipStream_t the next submit launches H2D, scale and k_encode on (for event timing by
+ * the caller; the tail kernels run on another stream ordered after k_encode).  With
+ * -huffman optimal or -vf scale consecutive submits alternate between two such streams. */
 void *mjg_stream(mjg_ctx *ctx);
 
 /* Pinned host memory for mjg_submit / mjg_fetch. */
