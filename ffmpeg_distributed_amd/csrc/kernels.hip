@@ -1741,11 +1741,13 @@ __device__ __forceinline__ void group_values(const GroupWords &g, uint32_t kb, u
   int base = __popcll(__ballot(lane >= 1 && lane < g.n && rsw < wk));
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   int own[R];
-  const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
 #pragma unroll
   for (int i = 0; i < R; i++) {
-    const uint64_t m = __ballot(marks[64 * i + lane] != 0);
-    own[i] = base + __popcll(m & le);
+    const uint32_t mark = marks[64 * i + lane];
+    const uint64_t m = __ballot(mark != 0);
+    // chunk starts at or before the lane's word: mbcnt counts the ballot bits below the lane
+    own[i] = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
+             (int)mark;
     base += __popcll(m);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1777,11 +1779,15 @@ __device__ __forceinline__ void group_values(const GroupWords &g, uint32_t kb, u
     X[i] = nX ? X[i] : 0u;
     B[i] = nB ? B[i] : 0u;
 #else
-    const uint32_t *slot = g.slot0 + (size_t)(uint32_t)c * kSlotWords;
-    A[i] = slot[wi];
-    X[i] = (bnd[i] && off && rem > 32u - off) ? slot[wi + 1] : 0u;
+    // 32-bit offsets from the group's first slot (the wave-uniform base: saddr loads)
+    const uint8_t *s0 = (const uint8_t *)g.slot0;  // byte offsets < 2^32: one 32-bit VGPR each
+    const uint32_t oa = (__umul24((uint32_t)c, (uint32_t)kSlotWords) + wi) << 2;
+    A[i] = *(const uint32_t *)(s0 + oa);
+    X[i] = (bnd[i] && off && rem > 32u - off) ? *(const uint32_t *)(s0 + oa + 4u) : 0u;
     const bool has_next = (inf[i] >> 27) & 1u;
-    B[i] = (own_nx[i] && (!bnd[i] || (rem < 32u && has_next))) ? slot[bnd[i] ? (uint32_t)kSlotWords : wi + 1] : 0u;
+    B[i] = (own_nx[i] && (!bnd[i] || (rem < 32u && has_next)))
+               ? *(const uint32_t *)(s0 + (bnd[i] ? __umul24((uint32_t)c + 1u, (uint32_t)kSlotWords * 4u) : oa + 4u))
+               : 0u;
 #endif
   }
 #pragma unroll
@@ -1836,12 +1842,12 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
                                                   uint32_t *__restrict__ group_ff, int nchunks, int gps,
                                                   int ngroups, uint32_t *__restrict__ stream) {
   __shared__ uint8_t s_marks[4][64 * kTailRounds];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int gi = blockIdx.x * 4 + wave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int gi = blockIdx.x * 4 + wave;  // wave-uniform: the group's pointers are scalar
   for (int i = lane; i < 64 * kTailRounds; i += 64) s_marks[wave][i] = 0;
   if (gi >= ngroups) return;
   const GroupWords g = group_words(scratch, chunk_bits, chunk_off, seg_bits, nchunks, gps, gi, lane);
-  uint32_t *sw = stream + (size_t)g.s * nchunks * kSlotWords;  // the segment's realigned words
+  uint8_t *sw = (uint8_t *)(stream + (size_t)g.s * nchunks * kSlotWords);  // the segment's realigned words
   uint32_t cnt = 0;
   for (uint32_t kb = g.k0; kb < g.k1; kb += 64 * kTailRounds) {
     uint32_t v[kTailRounds];
@@ -1852,7 +1858,7 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
       if (k < g.k1) {
         cnt += ff_bytes(v[i]);
 #ifndef MJG_EXP_COUNT_NOSTREAM
-        sw[k] = v[i];
+        *(uint32_t *)(sw + 4u * k) = v[i];
 #endif
       }
     }
@@ -1979,7 +1985,7 @@ __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ hdr_lens, int dht_pos, int dht_end, const uint8_t *__restrict__ dht,
     const uint32_t *__restrict__ dht_nval, uint8_t *__restrict__ out, uint64_t out_cap,
     uint32_t *__restrict__ status) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int gi = blockIdx.x * 4 + wave, ngroups = gps * nseg * nframes;
   if (gi >= ngroups) return;
   const int s = gi / gps, gx = gi - s * gps, f = s / nseg, si = s - f * nseg;
@@ -2001,13 +2007,13 @@ __global__ __launch_bounds__(256) void k_write(
     m[0] = 0xff;
     m[1] = si == nseg - 1 ? 0xd9 : (uint8_t)(0xd0 + (si & 7));
   }
-  const uint32_t *sw = stream + i0 * kSlotWords;
+  const uint8_t *sw = (const uint8_t *)(stream + i0 * kSlotWords);
   uint8_t *ob = out + sbase + ff_off[gi];  // + 4 k + the word's 0xFF prefix in the group
   uint32_t carry = 0;
   for (uint32_t kb = k0; kb < k1; kb += 64 * kTailRounds) {
     uint32_t v[kTailRounds];
 #pragma unroll
-    for (int i = 0; i < kTailRounds; i++) v[i] = sw[min(kb + 64 * i + lane, k1 - 1)];
+    for (int i = 0; i < kTailRounds; i++) v[i] = *(const uint32_t *)(sw + 4u * min(kb + 64 * i + lane, k1 - 1));
 #pragma unroll
     for (int i = 0; i < kTailRounds; i++) {
       if (kb + 64 * i >= k1) break;  // wave-uniform
