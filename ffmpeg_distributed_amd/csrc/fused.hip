@@ -303,6 +303,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];
   __shared__ uint8_t s_zz[64];
+  __shared__ uint2 s_zd[64];  // zigzag -> exact_coef descriptor (zz_desc)
   __shared__ __attribute__((aligned(16))) float s_thr[64];
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];
   __shared__ uint8_t s_scat[64];
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
+    s_zd[tid] = zz_desc(tid, tabs);
     s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
       s_m2[tid] = (uint32_t)(uint16_t)kPass2Dot[2 * tid] | ((uint32_t)(uint16_t)kPass2Dot[2 * tid + 1] << 16);
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
       const size_t t = (size_t)frame * g.nchunks + chunk;
       if (MODE == kCount) {
         CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + t * kSymCap * 64 + lane};
-        if (active) emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
+        if (active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
         if (chunk < g.nchunks) symn[t * 64 + lane] = cs.n;
       } else {
         ShiftSink q;
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
         q.dct = s_dc + tab * 16;
         q.stage = stage;
         if (active) {
-          emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
+          emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);
           if (q.bits > 128) q.flush();
         }
         if (chunk < g.nchunks) pack_chunk(q, active, scratch + t * kSlotWords, chunk_bits + t, lane);

@@ -208,6 +208,16 @@ __device__ __forceinline__ int dc_cat(int diff) {
   return diff == 0 ? 0 : 32 - __clz(a);
 }
 
+// JPEG magnitude category and mantissa of v != 0 (mjpegenc.c encode_block: mant = v, or v - 1
+// for v < 0, in `cat` bits): t = v - (v < 0) holds the mantissa in its low bits, and cat is
+// where t's bits start to differ from its sign (clrsb: v_ffbh_i32), so |v| is never formed.
+__device__ __forceinline__ int mag_cat(int v, uint32_t &mant) {
+  const int t = v + (v >> 31);
+  const int cat = 31 - __builtin_clrsb(t);  // v_ffbh_i32
+  mant = __builtin_amdgcn_ubfe((uint32_t)t, 0u, (uint32_t)cat);
+  return cat;
+}
+
 // The emission pass: the block's last 128 bits right-aligned in a 4-register shift register
 // (w3 lowest; the block's offset in the chunk is not known yet), and the total bit count.
 // Appending n <= 26 bits is four funnel shifts, (w_i << n) | (w_i+1 >> (32 - n)), one
@@ -282,6 +292,34 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
   return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
 }
 
+// exact_coef for zigzag position k from its descriptor (zz_desc, in LDS): x = the v_perm
+// selector of the column's u16 half, y = qmat | (column / 2) << 18 | row << 20 | DC-row flag
+// << 23 (rows 0 and 4: the pass-2 sums only).  One 8-byte LDS read per candidate instead of the
+// zigzag and qmat table reads and the index arithmetic.
+__device__ __forceinline__ uint2 zz_desc(int k, const uint32_t *tabs) {
+  const int n = kZigzag[k], ro = n >> 3, c = n & 7;
+  return make_uint2((c & 1) ? 0x07060302u : 0x05040100u,
+                    tabs[544 + c * 8 + ro] | (uint32_t)(c >> 1) << 18 | (uint32_t)ro << 20 |
+                        (uint32_t)((ro & 3) == 0) << 23);
+}
+__device__ __forceinline__ int exact_coef_d(const uint32_t *pkcol, uint2 d, const uint32_t *m2p) {
+  const uint32_t *col = pkcol + ((d.y >> 18) & 3u) * 64;
+  const uint4 mp = *(const uint4 *)(m2p + ((d.y >> 20) & 7u) * 4);
+  const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
+  const bool dc_row = (d.y >> 23) & 1u;
+  int acc = dc_row ? 8 : (1 << 16);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t w0 = col[((2 * i) * 4) * 64], w1 = col[((2 * i + 1) * 4) * 64];
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x) ^ 0x80008000u;
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
+                                 false);
+  }
+  const int u = acc >> (dc_row ? 4 : 17);
+  const int qm = (int)(d.y & 0x3ffffu);
+  return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
+}
+
 // Bit-pack one block's Huffman codes, FFmpeg mjpegenc.c encode_block /
 // mjpegenc_common.c ff_mjpeg_encode_dc (ZRL 0xF0 per 16 zeros, EOB unless coef 63 != 0).
 // `cand` is a superset of the nonzero AC positions in zigzag order (the float screening of
@@ -297,20 +335,20 @@ __device__ __forceinline__ void emit_ac(int k, int v, int &prev, Sink &sink) {
     sink.ac(0xf0, 0, 0u);  // ZRL
     run -= 16;
   }
-  const int a = v < 0 ? -v : v;
-  const int cat = 32 - __clz(a);
-  sink.ac(((run & 15) << 4) | cat, cat, (uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u));
+  uint32_t mant;
+  const int cat = mag_cat(v, mant);
+  sink.ac(((run & 15) << 4) | cat, cat, mant);
 }
 
 // Candidates are taken two at a time so the LDS reads of both (zigzag -> natural index,
 // the column of the row image, the quantiser) are in flight together.
 template <class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
-                                           const uint8_t *zz, const uint32_t *m2, const int *qc,
-                                           Sink &sink) {
+                                           const uint2 *zd, const uint32_t *m2, Sink &sink) {
   {
-    const int cat = dc_cat(diff);
-    sink.dc(cat, (uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << cat) - 1u));
+    uint32_t mant = 0;
+    const int cat = diff ? mag_cat(diff, mant) : 0;
+    sink.dc(cat, mant);
   }
   int prev = 0;
   while (cand) {
@@ -319,8 +357,8 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
     const bool two = cand != 0;
     const int k2 = two ? (int)__builtin_ctzll(cand) : k1;
     cand &= cand - 1;  // no-op when cand == 0
-    const int v1 = exact_coef(pkcol, zz[k1], m2, qc);
-    const int v2 = exact_coef(pkcol, zz[k2], m2, qc);
+    const int v1 = exact_coef_d(pkcol, zd[k1], m2);
+    const int v2 = exact_coef_d(pkcol, zd[k2], m2);
     emit_ac(k1, v1, prev, sink);
     if (two) emit_ac(k2, v2, prev, sink);
   }
@@ -339,25 +377,25 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
 //                 lane), which then go to block h's staging column (pack_chunk reads it)
 // Returns the block's bit count.  Same bytes as emit_block (FFmpeg encode_block).
 __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, int diff_h, int tab_h,
-                                                 const uint8_t *zz, const uint32_t *m2, const int *qc,
+                                                 const uint2 *zd, const uint32_t *m2,
                                                  const uint32_t *s_ac, const uint32_t *s_dc, uint32_t *s_hv,
                                                  uint32_t *stage_w, int lane) {
   const uint32_t wv = lane < 32 ? s_pk[lane * 64 + h] : 0u;
-  const int n = zz[lane], ro = n >> 3, c = n & 7;
-  const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
-  const uint4 mp = *(const uint4 *)(m2 + ro * 4);
+  const uint2 d = zd[lane];
+  const uint32_t cc = (d.y >> 18) & 3u;  // column pair
+  const uint4 mp = *(const uint4 *)(m2 + ((d.y >> 20) & 7u) * 4);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  const bool dc_row = ro == 0 || ro == 4;
+  const bool dc_row = (d.y >> 23) & 1u;
   int acc = dc_row ? 8 : (1 << 16);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i) * 4 + (c >> 1)) << 2), (int)wv);
-    const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i + 1) * 4 + (c >> 1)) << 2), (int)wv);
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel) ^ 0x80008000u;
+    const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i) * 4 + cc) << 2), (int)wv);
+    const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i + 1) * 4 + cc) << 2), (int)wv);
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x) ^ 0x80008000u;
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc, false);
   }
   const int u = acc >> (dc_row ? 4 : 17);
-  int v = (__mul24(u, qc[c * 8 + ro]) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
+  int v = (__mul24(u, (int)(d.y & 0x3ffffu)) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
   if (lane == 0) v = 0;  // the DC is coded from diff_h
   const uint64_t nz = __ballot(v != 0);
   const uint32_t *act = s_ac + tab_h * 256;
@@ -375,11 +413,11 @@ __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, in
         run -= 16;
       }
     }
-    const int a = v < 0 ? -v : v;
-    const int cat = 32 - __clz(a);
+    uint32_t mant;
+    const int cat = mag_cat(v, mant);
     const uint32_t e = act[((run & 15) << 4) | cat];
     const uint32_t cl = (e >> 16) + (uint32_t)cat;
-    V = (V << cl) | (((e & 0xffffu) << cat) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << cat) - 1u)));
+    V = (V << cl) | (((e & 0xffffu) << cat) | mant);
     L += cl;
   } else if (lane == 63) {  // EOB: coefficient 63 is zero
     const uint32_t e = act[0x00];
@@ -1079,6 +1117,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
+  __shared__ uint2 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
   constexpr bool SCR = !MF;  // the VALU column screen
   __shared__ __attribute__((aligned(16))) float s_thr[SCR ? 64 : 4];  // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
@@ -1099,6 +1138,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
+    s_zd[tid] = zz_desc(tid, tabs);
     if (SCR) s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
       s_m2[tid] = (uint32_t)(uint16_t)kPass2Dot[2 * tid] | ((uint32_t)(uint16_t)kPass2Dot[2 * tid + 1] << 16);
@@ -1223,7 +1263,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     }
     if (MODE == kCount) {
       CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kSymCap * 64 + lane};
-      if (cur_active) emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, cs);
+      if (cur_active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
       symn[(size_t)t * 64 + lane] = cs.n;
       if (tn < 0) break;
       if (new_batch) {
@@ -1240,14 +1280,14 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     q.stage = stage_w + lane;
     const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);
     if (cur_active && !((wide >> lane) & 1ull)) {
-      emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);
+      emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);
       if (q.bits > 128) q.flush();
     }
     if (wide) {  // the heavy blocks, one wave-parallel block at a time
       for (uint64_t hw = wide; hw; hw &= hw - 1) {
         const int h = (int)__builtin_ctzll(hw);
         const uint32_t nb = emit_block_wave(s_pk, h, __builtin_amdgcn_readlane(diff, h),
-                                            __builtin_amdgcn_readlane(tab, h), s_zz, s_m2, s_qc, s_ac, s_dc,
+                                            __builtin_amdgcn_readlane(tab, h), s_zd, s_m2, s_ac, s_dc,
                                             s_hv, stage_w, lane);
         if (lane == h) {
           q.bits = nb;
