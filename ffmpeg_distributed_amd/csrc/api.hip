@@ -275,7 +275,7 @@ void free_ctx(mjg_ctx *c) {
   if (c->h_fetch) (void)hipHostFree(c->h_fetch);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
-  if (c->tail) (void)hipStreamDestroy(c->tail);
+  if (c->tail && c->tail != c->stream) (void)hipStreamDestroy(c->tail);
   delete c;
 }
 
@@ -558,7 +558,11 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+#ifdef MJG_EXP_SERIAL_TAIL  // A/B: the tail on the submit stream (no co-run with the next k_encode)
+  c->tail = c->stream;
+#else
   HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));
+#endif
 
   c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
   const int cf = k.chroma_format;

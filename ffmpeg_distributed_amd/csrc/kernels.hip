@@ -616,7 +616,10 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
 // counters: c2 -6%, c5 -5% against 16; 8 and 24 measured too), 8 for the MFMA stage (3 waves
 // per SIMD, fewer chunks per wave), each the faster on its BASELINE configs
 template <bool MF>
-constexpr int kBatchOf = MF ? 8 : 12;
+#ifndef MJG_EXP_BATCH
+#define MJG_EXP_BATCH 12
+#endif
+constexpr int kBatchOf = MF ? 8 : MJG_EXP_BATCH;
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
 // quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
@@ -797,7 +800,9 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
     for (int j = 0; j < 4; j++)
       s_pk[(r * 4 + j) * 64 + lane] =
           __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
+#ifndef MJG_EXP_NO_SB_ROW
     __builtin_amdgcn_sched_barrier(0);
+#endif
   }}
 
   // Column pass (jfdctint pass 2) as a float *screen*: the products of pass 2 need up to
@@ -811,7 +816,9 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
                                               const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb) {
 #pragma unroll
   for (int jp = 0; jp < 4; jp++) {
+#ifndef MJG_EXP_NO_SB_PAIR
     __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
+#endif
     uint32_t w[8];
 #pragma unroll
     for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
@@ -839,7 +846,9 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
+#ifndef MJG_EXP_NO_SB_COL
       __builtin_amdgcn_sched_barrier(0);  // one column at a time
+#endif
       const int col = 2 * jp + h;
       if (h ? skip1 : skip0) {  // wave-uniform: 8 zero screen bits
         if (col < 4)

@@ -61,8 +61,11 @@ def main():
                                   dct_mfma=True if name.endswith("_m") else False if name.endswith("_v") else None)
     res = {n: [] for n in encs}
     ref = None
+    names = list(encs)
     for rnd in range(6):
-        for n, e in encs.items():
+        # rotate the order every round: no variant always runs first (or right after another)
+        for n in names[rnd % len(names):] + names[:rnd % len(names)]:
+            e = encs[n]
             e.kernel_times(reset=True)
             for _ in range(3):
                 e.submit(device_ptr=pool.data_ptr(), nframes=N)
