@@ -845,17 +845,25 @@ void launch_fused(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
     range ? launch_fused3<4, 3, true, MODE>(c, S, src, n) : launch_fused3<4, 3, false, MODE>(c, S, src, n);
 }
 
-template <int MODE, bool MF>
-void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+template <int MODE, bool MF, bool DBG>
+void launch_encode3(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
   if (g.range_convert)
-    k_encode<true, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
+    k_encode<true, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         S.d_stage_bits, S.d_syms, S.d_symn);
   else
-    k_encode<false, MODE, MF><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
+    k_encode<false, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         S.d_stage_bits, S.d_syms, S.d_symn);
+}
+
+template <int MODE, bool MF>
+void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+  if (c->geom.debug_coefs)
+    launch_encode3<MODE, MF, true>(c, S, enc_in, wgs, ntasks);
+  else
+    launch_encode3<MODE, MF, false>(c, S, enc_in, wgs, ntasks);
 }
 
 // The DCT stage: the VALU passes, or (-huffman default) dct_mfma.

@@ -1115,7 +1115,9 @@ struct XcdUnits {
 };
 
 // MF: the DCT stage on the matrix cores (dct_mfma) instead of row_pass + column_screen.
-template <bool RC, int MODE, bool MF = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
+// DBG: the MJG_F_DEBUG_COEFS instantiation (quantised blocks out); the product kernels carry
+// neither its branch nor its live scalars (k_encode is short of SGPRs: they spill to VGPR lanes).
+template <bool RC, int MODE, bool MF = false, bool DBG = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
@@ -1241,7 +1243,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
     if (cur_active) {
       if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
-      if (g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
+      if (DBG && g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
 #pragma unroll 1
