@@ -476,6 +476,33 @@ def test_pipelined_submits():
     assert a + b == oracle_frames(nz, 256, 128, 2, True)
 
 
+@pytest.mark.parametrize("cfg", ["optimal", "scale", "scale_optimal", "default"])
+def test_pipelined_submits_two_streams(cfg):
+    """-huffman optimal and -vf scale contexts run their two slots on two streams (their
+    chains of launches overlap, csrc/api.hip alloc_slot; a default-table context keeps one
+    stream): five submits, two queued at a time so every slot is reused on its own stream, from
+    host memory (per-slot H2D staging) and with ragged batches; every frame byte-equal to the
+    oracle."""
+    sw, sh = 200, 120
+    dw, dh = (100, 60) if cfg.startswith("scale") else (sw, sh)
+    huffman = "optimal" if cfg.endswith("optimal") else "default"
+    frames = rand_frames(sw, sh, 13, seed=77, kind="testsrc")
+    ref = oracle_frames(frames, sw, sh, 4, False, dw, dh, huffman=huffman)
+    cuts = [(0, 3), (3, 5), (5, 8), (8, 11), (11, 13)]
+    got = []
+    with MjpegEncoder(0, sw, sh, dw, dh, qscale=4, max_batch=3, huffman=huffman) as enc:
+        for i, (a, b) in enumerate(cuts):
+            enc.submit(frames[a:b])
+            if i >= 1:
+                enc.sync()
+                got += enc.fetch()
+        enc.sync()
+        got += enc.fetch()
+    assert len(got) == len(ref)
+    for i in range(len(ref)):
+        assert got[i] == ref[i], (cfg, i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
 def _sweep_cases(seed=2026, n=600, wmax=420, hmax=260, nmax=3):
     """Seeded random configurations over every option of the GPU profile at once."""
     rng = np.random.default_rng(seed)
