@@ -303,10 +303,10 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];
   __shared__ uint8_t s_zz[64];
-  __shared__ uint2 s_zd[64];  // zigzag -> exact_coef descriptor (zz_desc)
+  __shared__ uint4 s_zd[64];  // zigzag -> exact_coef descriptor (zz_desc)
   __shared__ __attribute__((aligned(16))) float s_thr[64];
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];
-  __shared__ uint8_t s_scat[64];
+  __shared__ uint8_t s_scat[68];
   __shared__ uint32_t s_desc[8];
   __shared__ uint32_t s_skip[12];
   __shared__ int s_dcx[2][kFusedWaves][8];  // per group parity: each chunk's last 8 DCs
@@ -323,8 +323,9 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
     s_zd[tid] = zz_desc(tid, tabs);
     s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
-      s_m2[tid] = (uint32_t)(uint16_t)kPass2Dot[2 * tid] | ((uint32_t)(uint16_t)kPass2Dot[2 * tid + 1] << 16);
+      s_m2[tid] = pass2_pair(tid);
     s_scat[tid] = kScreenScatter[tid];
+    if (tid < 4) s_scat[64 + tid] = 0;
   }
   if (tid < 8) s_desc[tid] = tabs[672 + tid];
   if (tid < 12) s_skip[tid] = tabs[680 + tid];
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
         q.stage = stage;
         if (active) {
           emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);
-          if (q.bits > 128) q.flush();
+          q.finish();
         }
         if (chunk < g.nchunks) pack_chunk(q, active, scratch + t * kSlotWords, chunk_bits + t, lane);
       }

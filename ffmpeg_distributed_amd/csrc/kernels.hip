@@ -56,6 +56,14 @@ constexpr float kRnd = 0x1p-10f;
    4433, -10704, 10704, -4433, -4433, 10704, -10704, 4433,             \
    2260, -6436, 9633, -11363, 11363, -9633, 6436, -2260}
 __device__ static constexpr int kPass2Dot[64] = MJG_PASS2_DOT;
+// The kernel's pass-2 rows (s_m2): rows 0 and 4 scaled by 2^13, so every row is accumulated
+// from 2^16 and descaled by 17 (2^13 (S + 8) >> 17 == (S + 8) >> 4; |S| <= 8 * 32640, so
+// 2^13 (S + 8) stays below 2^31): no per-row start value or shift in exact_coef.
+constexpr int kPass2DcScale = 8192;
+__device__ __forceinline__ uint32_t pass2_pair(int i) {  // int16 pair of entries 2i, 2i + 1
+  const int r = i >> 2, f = (r & 3) == 0 ? kPass2DcScale : 1;
+  return (uint32_t)(uint16_t)(kPass2Dot[2 * i] * f) | ((uint32_t)(uint16_t)(kPass2Dot[2 * i + 1] * f) << 16);
+}
 // k_encode screen bit -> zigzag scan position.  Columns 0-3 (DC excluded) are shifted
 // into word A in the order col-major (col, row), columns 4-7 into word B, so the j-th
 // coefficient screened lands at bit 30-j (A) / 31-j (B).
@@ -218,6 +226,14 @@ __device__ __forceinline__ int mag_cat(int v, uint32_t &mant) {
   return cat;
 }
 
+// v_ffbh_i32: the bit position, counted from the MSB, of the first bit that differs from the
+// sign bit; -1 for 0 and -1.  For t = v - (v < 0) of a nonzero v, 32 - ffbh is the category.
+__device__ __forceinline__ int ffbh_i32(int t) {
+  int r;
+  asm("v_ffbh_i32 %0, %1" : "=v"(r) : "v"(t));
+  return r;
+}
+
 // The emission pass: the block's last 128 bits right-aligned in a 4-register shift register
 // (w3 lowest; the block's offset in the chunk is not known yet), and the total bit count.
 // Appending n <= 26 bits is four funnel shifts, (w_i << n) | (w_i+1 >> (32 - n)), one
@@ -228,8 +244,9 @@ __device__ __forceinline__ int mag_cat(int v, uint32_t &mant) {
 struct ShiftSink {
   MJG_SINK_SYMBOLS
   uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-  uint32_t bits = 0;
-  uint32_t spilled = 0;  // stream bits already staged (multiple of 32); bits - spilled <= 128
+  uint32_t bits = 0;     // stream bits (set by finish(), or by emit_block_wave)
+  int room = 128;        // free window bits: 128 - (stream bits - spilled)
+  uint32_t spilled = 0;  // stream bits already staged (multiple of 32)
   bool staged = false;   // the whole stream is in the staging column (emit_block_wave)
   uint32_t *stage;
   // the staged word at stream bit `spilled`: window offset o = 128 - (bits - spilled) from the top
@@ -237,18 +254,23 @@ struct ShiftSink {
     return o ? __builtin_amdgcn_alignbit(a, b, 32u - o) : a;
   }
   __device__ __forceinline__ void emit(uint32_t v, int n) {
-    if (bits + (uint32_t)n - spilled > 128u) {  // the oldest unstaged word would be shifted out
-      stage[(spilled >> 5) * 64] = window_word(128u - (bits - spilled), w0, w1);
+    room -= n;
+    if (room < 0) {  // the oldest unstaged word would be shifted out
+      stage[(spilled >> 5) * 64] = window_word((uint32_t)(room + n), w0, w1);
       spilled += 32;
+      room += 32;
     }
     const uint32_t sh = 32u - (uint32_t)n;
     w0 = __builtin_amdgcn_alignbit(w0, w1, sh);
     w1 = __builtin_amdgcn_alignbit(w1, w2, sh);
     w2 = __builtin_amdgcn_alignbit(w2, w3, sh);
-    w3 = __builtin_amdgcn_alignbit(w3, v << sh, sh);
-    bits += (uint32_t)n;
+    w3 = (w3 << n) | v;  // v_lshl_or (n <= 27)
   }
-  __device__ __forceinline__ void finish() {}
+  // the block's bit count; a block past 128 bits stages the rest of its window
+  __device__ __forceinline__ void finish() {
+    bits = spilled + 128u - (uint32_t)room;
+    if (bits > 128u) flush();
+  }
   // a block past 128 bits: stage the words still in the window (stream words
   // spilled/32 .. (bits-1)/32, at most 4)
   __device__ __forceinline__ void flush() {
@@ -278,8 +300,7 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
   const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
   const uint4 mp = *(const uint4 *)(m2p + ro * 4);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  const bool dc_row = ro == 0 || ro == 4;
-  int acc = dc_row ? 8 : (1 << 16);
+  int acc = 1 << 16;  // rows 0 / 4 scaled (pass2_pair)
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t w0 = pkcol[((2 * i) * 4 + (c >> 1)) * 64], w1 = pkcol[((2 * i + 1) * 4 + (c >> 1)) * 64];
@@ -287,27 +308,26 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
                                  false);
   }
-  const int u = acc >> (dc_row ? 4 : 17);
+  const int u = acc >> 17;
   const int qm = qc[c * 8 + ro];
   return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
 }
 
-// exact_coef for zigzag position k from its descriptor (zz_desc, in LDS): x = the v_perm
-// selector of the column's u16 half, y = qmat | (column / 2) << 18 | row << 20 | DC-row flag
-// << 23 (rows 0 and 4: the pass-2 sums only).  One 8-byte LDS read per candidate instead of the
-// zigzag and qmat table reads and the index arithmetic.
-__device__ __forceinline__ uint2 zz_desc(int k, const uint32_t *tabs) {
+// exact_coef for zigzag position k from its descriptor (zz_desc, in LDS), returned as
+// t = v - (v < 0) (see emit_ac): x = the v_perm selector of the column's u16 half, y = qmat,
+// z = the pass-2 row's byte offset in s_m2, w = the column pair's byte offset in the row
+// image.  One 16-byte LDS read per candidate replaces the zigzag, qmat and row tables and
+// every field extraction.
+__device__ __forceinline__ uint4 zz_desc(int k, const uint32_t *tabs) {
   const int n = kZigzag[k], ro = n >> 3, c = n & 7;
-  return make_uint2((c & 1) ? 0x07060302u : 0x05040100u,
-                    tabs[544 + c * 8 + ro] | (uint32_t)(c >> 1) << 18 | (uint32_t)ro << 20 |
-                        (uint32_t)((ro & 3) == 0) << 23);
+  return make_uint4((c & 1) ? 0x07060302u : 0x05040100u, tabs[544 + c * 8 + ro], (uint32_t)ro * 16u,
+                    (uint32_t)(c >> 1) * 256u);
 }
-__device__ __forceinline__ int exact_coef_d(const uint32_t *pkcol, uint2 d, const uint32_t *m2p) {
-  const uint32_t *col = pkcol + ((d.y >> 18) & 3u) * 64;
-  const uint4 mp = *(const uint4 *)(m2p + ((d.y >> 20) & 7u) * 4);
+__device__ __forceinline__ int exact_coef_t(const uint32_t *pkcol, uint4 d, const uint32_t *m2p) {
+  const uint32_t *col = (const uint32_t *)((const uint8_t *)pkcol + d.w);
+  const uint4 mp = *(const uint4 *)((const uint8_t *)m2p + d.z);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  const bool dc_row = (d.y >> 23) & 1u;
-  int acc = dc_row ? 8 : (1 << 16);
+  int acc = 1 << 16;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t w0 = col[((2 * i) * 4) * 64], w1 = col[((2 * i + 1) * 4) * 64];
@@ -315,9 +335,9 @@ __device__ __forceinline__ int exact_coef_d(const uint32_t *pkcol, uint2 d, cons
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
                                  false);
   }
-  const int u = acc >> (dc_row ? 4 : 17);
-  const int qm = (int)(d.y & 0x3ffffu);
-  return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
+  const int u = acc >> 17;
+  // t = v - (v < 0) (mag_cat's t) directly: for u < 0 the rounding constant less 2^21
+  return (__mul24(u, (int)d.y) + (u < 0 ? -1 - (3 << 18) : (3 << 18))) >> 21;
 }
 
 // Bit-pack one block's Huffman codes, FFmpeg mjpegenc.c encode_block /
@@ -326,17 +346,20 @@ __device__ __forceinline__ int exact_coef_d(const uint32_t *pkcol, uint2 d, cons
 // the column pass); each candidate is quantised exactly and skipped when it is zero, so
 // runs and EOB are those of the exact block.  (Mean nonzero AC per block is ~1.3 on
 // testsrc2 4K q5, so the loop is short.)
+// t: the coefficient v as v - (v < 0) (exact_coef_t), so t is 0 or -1 exactly when v == 0
+// and the category is 32 - v_ffbh_i32(t) (no |v|, no sign fix-up).
 template <class Sink>
-__device__ __forceinline__ void emit_ac(int k, int v, int &prev, Sink &sink) {
-  if (v == 0) return;  // screened in, quantises to zero
+__device__ __forceinline__ void emit_ac(int k, int t, int &prev, Sink &sink) {
+  const int fb = ffbh_i32(t);
+  if (fb < 0) return;  // screened in, quantises to zero
   int run = k - prev - 1;
   prev = k;
   while (run >= 16) {
     sink.ac(0xf0, 0, 0u);  // ZRL
     run -= 16;
   }
-  uint32_t mant;
-  const int cat = mag_cat(v, mant);
+  const int cat = 32 - fb;
+  const uint32_t mant = __builtin_amdgcn_ubfe((uint32_t)t, 0u, (uint32_t)cat);
   sink.ac(((run & 15) << 4) | cat, cat, mant);
 }
 
@@ -344,7 +367,7 @@ __device__ __forceinline__ void emit_ac(int k, int v, int &prev, Sink &sink) {
 // the column of the row image, the quantiser) are in flight together.
 template <class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
-                                           const uint2 *zd, const uint32_t *m2, Sink &sink) {
+                                           const uint4 *zd, const uint32_t *m2, Sink &sink) {
   {
     uint32_t mant = 0;
     const int cat = diff ? mag_cat(diff, mant) : 0;
@@ -357,10 +380,10 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
     const bool two = cand != 0;
     const int k2 = two ? (int)__builtin_ctzll(cand) : k1;
     cand &= cand - 1;  // no-op when cand == 0
-    const int v1 = exact_coef_d(pkcol, zd[k1], m2);
-    const int v2 = exact_coef_d(pkcol, zd[k2], m2);
-    emit_ac(k1, v1, prev, sink);
-    if (two) emit_ac(k2, v2, prev, sink);
+    const int t1 = exact_coef_t(pkcol, zd[k1], m2);
+    const int t2 = exact_coef_t(pkcol, zd[k2], m2);
+    emit_ac(k1, t1, prev, sink);
+    if (two) emit_ac(k2, t2, prev, sink);
   }
   if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB
 }
@@ -377,16 +400,15 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
 //                 lane), which then go to block h's staging column (pack_chunk reads it)
 // Returns the block's bit count.  Same bytes as emit_block (FFmpeg encode_block).
 __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, int diff_h, int tab_h,
-                                                 const uint2 *zd, const uint32_t *m2,
+                                                 const uint4 *zd, const uint32_t *m2,
                                                  const uint32_t *s_ac, const uint32_t *s_dc, uint32_t *s_hv,
                                                  uint32_t *stage_w, int lane) {
   const uint32_t wv = lane < 32 ? s_pk[lane * 64 + h] : 0u;
-  const uint2 d = zd[lane];
-  const uint32_t cc = (d.y >> 18) & 3u;  // column pair
-  const uint4 mp = *(const uint4 *)(m2 + ((d.y >> 20) & 7u) * 4);
+  const uint4 d = zd[lane];
+  const uint32_t cc = d.w >> 8;  // column pair
+  const uint4 mp = *(const uint4 *)((const uint8_t *)m2 + d.z);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  const bool dc_row = (d.y >> 23) & 1u;
-  int acc = dc_row ? 8 : (1 << 16);
+  int acc = 1 << 16;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i) * 4 + cc) << 2), (int)wv);
@@ -394,14 +416,15 @@ __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, in
     const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x) ^ 0x80008000u;
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc, false);
   }
-  const int u = acc >> (dc_row ? 4 : 17);
-  int v = (__mul24(u, (int)(d.y & 0x3ffffu)) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
-  if (lane == 0) v = 0;  // the DC is coded from diff_h
-  const uint64_t nz = __ballot(v != 0);
+  const int u = acc >> 17;
+  int t = (__mul24(u, (int)d.y) + (u < 0 ? -1 - (3 << 18) : (3 << 18))) >> 21;  // exact_coef_t
+  if (lane == 0) t = 0;  // the DC is coded from diff_h
+  const int fb = ffbh_i32(t);
+  const uint64_t nz = __ballot(fb >= 0);
   const uint32_t *act = s_ac + tab_h * 256;
   uint64_t V = 0;
   uint32_t L = 0;
-  if (v != 0) {
+  if (fb >= 0) {
     const uint64_t below = nz & ((1ull << lane) - 1ull);
     int run = lane - (below ? 63 - (int)__builtin_clzll(below) : 0) - 1;
     if (run >= 16) {
@@ -413,8 +436,8 @@ __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, in
         run -= 16;
       }
     }
-    uint32_t mant;
-    const int cat = mag_cat(v, mant);
+    const int cat = 32 - fb;
+    const uint32_t mant = __builtin_amdgcn_ubfe((uint32_t)t, 0u, (uint32_t)cat);
     const uint32_t e = act[((run & 15) << 4) | cat];
     const uint32_t cl = (e >> 16) + (uint32_t)cat;
     V = (V << cl) | (((e & 0xffffu) << cat) | mant);
@@ -897,19 +920,19 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
 }
 
 // Candidate bits (column_screen) -> zigzag-ordered candidate mask (a handful per block).
+// One bit of each word per step, both table reads in flight together (one LDS round trip per
+// step, max(|A|, |B|) steps).  A word with no bit left reads a dummy entry: A's bit 31 is
+// never set (31 coefficients) and B's dummy is entry 64; both map to zigzag 0, the DC, which
+// is no candidate and is cleared at the end.
 __device__ __forceinline__ uint64_t screen_mask(uint32_t ca, uint32_t cb, const uint8_t *s_scat) {
   uint64_t mask = 0;
-  while (ca) {
-    const int pos = __builtin_ctz(ca);
+  while (ca | cb) {
+    const uint32_t pa = (uint32_t)__builtin_ctzg(ca, 31), pb = (uint32_t)__builtin_ctzg(cb, 32);
     ca &= ca - 1;
-    mask |= 1ull << s_scat[pos];
-  }
-  while (cb) {
-    const int pos = __builtin_ctz(cb);
     cb &= cb - 1;
-    mask |= 1ull << s_scat[32 + pos];
+    mask |= (1ull << s_scat[pa]) | (1ull << s_scat[32 + pb]);
   }
-  return mask;
+  return mask & ~1ull;
 }
 
 // DC predictor of this lane's block (FFmpeg last_dc, 128 at every segment start): the block
@@ -1128,11 +1151,11 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
-  __shared__ uint2 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
+  __shared__ uint4 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
   constexpr bool SCR = !MF;  // the VALU column screen
   __shared__ __attribute__((aligned(16))) float s_thr[SCR ? 64 : 4];  // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
-  __shared__ uint8_t s_scat[SCR ? 64 : 4];  // candidate bit -> zigzag index (kScreenScatter)
+  __shared__ uint8_t s_scat[SCR ? 68 : 4];  // candidate bit -> zigzag index (kScreenScatter; [64]: dummy)
   __shared__ uint8_t s_rc[RC ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint4 s_f[MF ? 12 * 64 : 1];  // MFMA A fragments (dct_mfma): [0, 2) pass 1, [4, 12) pass 2
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
@@ -1152,8 +1175,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     s_zd[tid] = zz_desc(tid, tabs);
     if (SCR) s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
-      s_m2[tid] = (uint32_t)(uint16_t)kPass2Dot[2 * tid] | ((uint32_t)(uint16_t)kPass2Dot[2 * tid + 1] << 16);
+      s_m2[tid] = pass2_pair(tid);
     if (SCR) s_scat[tid] = kScreenScatter[tid];
+    if (SCR && tid < 4) s_scat[64 + tid] = 0;
   }
   if (tid < 8) {
     s_desc[tid] = tabs[672 + tid];
@@ -1292,7 +1316,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);
     if (cur_active && !((wide >> lane) & 1ull)) {
       emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);
-      if (q.bits > 128) q.flush();
+      q.finish();
     }
     if (wide) {  // the heavy blocks, one wave-parallel block at a time
       for (uint64_t hw = wide; hw; hw &= hw - 1) {
@@ -1389,7 +1413,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
           q.ac((int)v, (int)(v & 15u), mant);
       }
     }
-    if (q.bits > 128) q.flush();
+    q.finish();
     pack_chunk(q, active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
   }
 }

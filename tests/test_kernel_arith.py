@@ -167,6 +167,23 @@ def test_pass2_dot_rows_equal_oracle_fdct():
             assert ((acc >> sh) == ref[:, c]).all(), (it, c)
 
 
+def test_pass2_scaled_dc_rows_equal_oracle_fdct():
+    """k_encode's s_m2 (pass2_pair): rows 0 and 4 scaled by kPass2DcScale, every row started
+    at 2^16 and descaled by 17, on signed row-pass values; int32 never wraps (extreme blocks)."""
+    scale = int(re.search(r"constexpr int kPass2DcScale = (\d+);", _src()).group(1))
+    dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
+    dot[[0, 4]] *= scale
+    rng = np.random.default_rng(5)
+    blocks = [np.full((8, 8), 255), np.zeros((8, 8), np.int64)]
+    blocks += [rng.choice([0, 255], (8, 8)) for _ in range(100)] + [rng.integers(0, 256, (8, 8)) for _ in range(200)]
+    for blk in blocks:
+        ref = oracle.fdct(blk.astype(np.int16)).reshape(8, 8).astype(np.int64)
+        img = pass1_f32(blk) - 32768
+        acc = dot @ img + (1 << 16)
+        assert (np.abs(acc) < 2 ** 31).all()
+        assert ((acc >> 17) == ref).all()
+
+
 def test_screen_thresholds_are_conservative():
     """Every coefficient that quantises to nonzero passes the fp32 screen (q = 1..31)."""
     dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)

@@ -25,17 +25,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
 
-EMIT = ("      emit_block(s_pk + lane, mask, diff, s_zz, s_m2, s_qc, q);\n"
-        "      if (q.bits > 128) q.flush();\n")
+EMIT = ("      emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);\n"
+        "      q.finish();\n")
 WIDE = "const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);"
-EXACT = "  const int ro = n >> 3, c = n & 7;\n  const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;\n  const uint4 mp"
+EXACT = "  const uint32_t *col = pkcol + ((d.y >> 18) & 3u) * 64;\n"
 SCREEN = "      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);"
 ROWPASS = "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);"
 
 SUBS = {
-    "noemit": [(EMIT, "      q.emit(((uint32_t)__popcll(mask) << 8) ^ ((uint32_t)diff & 255u), 16);\n"),
+    "noemit": [(EMIT, "      q.emit(((uint32_t)__popcll(mask) << 8) ^ ((uint32_t)diff & 255u), 16);\n"
+                      "      q.finish();\n"),
                (WIDE, "const uint64_t wide = 0;")],
-    "noexact": [(EXACT, "  if (n >= 0) return 1 + (n & 1);\n" + EXACT)],
+    "noexact": [(EXACT, "  if (d.x != 0u) return 1 + (int)(d.y & 1u);\n" + EXACT)],
     "noscreen": [(SCREEN, "      if (SCR) dc = (int)(s_pk[lane] & 255u) - 128;")],
     "nodct": [(ROWPASS, "      {\n#pragma unroll\n        for (int r = 0; r < 8; r++) {\n"
                         "          s_pk[(r * 4) * 64 + lane] = (uint32_t)raw[r];\n"

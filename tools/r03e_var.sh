@@ -8,7 +8,7 @@ mkdir -p $O
 VS=$(for v in $2; do printf "%s=:;" $v; done); VS=${VS%;}
 for wc in ${3:-c2:testsrc}; do
   w=${wc%%:*}; c=${wc##*:}
-  WL=$w CONTENT=$c VARIANTS="$VS" timeout -k 10 300 python3 tools/variants.py > $O/var_${w}_$c.txt 2>&1 || { tail -20 $O/var_${w}_$c.txt; exit 1; }
+  ROUNDS=${ROUNDS:-6} WL=$w CONTENT=$c VARIANTS="$VS" timeout -k 10 300 python3 tools/variants.py > $O/var_${w}_$c.txt 2>&1 || { tail -20 $O/var_${w}_$c.txt; exit 1; }
   echo "== $w $c"; grep -E "output|median" $O/var_${w}_$c.txt
 done
 echo done

@@ -62,7 +62,7 @@ def main():
     res = {n: [] for n in encs}
     ref = None
     names = list(encs)
-    for rnd in range(6):
+    for rnd in range(int(os.environ.get("ROUNDS", "6"))):
         # rotate the order every round: no variant always runs first (or right after another)
         for n in names[rnd % len(names):] + names[:rnd % len(names)]:
             e = encs[n]
