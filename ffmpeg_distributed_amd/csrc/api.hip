@@ -653,7 +653,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   //   others: |S| <= T 2^17 - 2^16 - 1             <= L1(row) R / 2
   // (T = ceil(5 2^18 / qmat) of that output, R = max - min of the column's row-pass values
   // u_r, S the pass-2 sum before DESCALE; dct_quantize_c gives 0 iff |DESCALE(S)| < T).  With
-  // U = u + 32768 (the u16 image): skip iff R <= Rmax, max U <= HI, min U >= LO.
+  // U = u + 16384 (the u16 image, columns 1-7): skip iff R <= Rmax, max U <= HI, min U >= LO.
   {
     static const int kDot[64] = MJG_PASS2_DOT;
     for (int jp = 1; jp < 4; jp++) {
@@ -675,7 +675,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
           }
         }
         rmax = std::max(0ll, rmax);
-        const long long hi = std::min(65535ll, 32768 + amax), lo = std::max(0ll, 32768 - amax);
+        const long long hi = std::min(65535ll, 16384 + amax), lo = std::max(0ll, 16384 - amax);
         lim[0] |= (uint32_t)rmax << (16 * h);
         lim[1] |= (uint32_t)hi << (16 * h);
         lim[2] |= (uint32_t)lo << (16 * h);

@@ -33,19 +33,20 @@ constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 bl
 #endif
 
 // fp32 exact-integer arithmetic (k_encode): adding kM = 1.5*2^23 rounds to an integer
-// (round-to-nearest-even) and keeps it in the low mantissa bits; kMb = kM + 32768 leaves
-// value + 32768 in the low 16 bits.  kRnd = 2^-10 turns floor(x/512 + 1/2) into RNE.
+// (round-to-nearest-even) and keeps it in the low mantissa bits; kMc = kM + 16384 leaves
+// value + 16384 in the low 16 bits.  kRnd = 2^-10 turns floor(x/512 + 1/2) into RNE.
+// The row image (s_pk) holds row-pass output 0 (the row sum, 0..32640) unbiased and outputs
+// 1-7 (|value| <= 16320) + 16384, so every u16 is below 2^15 and reads as the same value
+// when v_dot2_i32_i16 takes it as int16 (exact_coef: no sign fix-up).
 constexpr int kMfTabOff = 704;   // MF k_encode's f16 MFMA fragments (open_ctx, dct_mfma)
 constexpr int kTabWords = kMfTabOff + 12 * 64 * 4;  // device table block, see open_ctx
 constexpr float kM = 12582912.0f;
-constexpr float kMb = 12615680.0f;
+constexpr float kMc = 12599296.0f;  // kM + 16384: the row image's bias for outputs 1-7
 constexpr float kRnd = 0x1p-10f;
 
 // jfdctint pass 2 (CONST_BITS 13, PASS1_BITS 4) per output row as one dot product over
 // the 8 column inputs: the LLM butterfly's t/z terms multiplied out (rows 0/4: +-1 with
-// DESCALE 4; others: DESCALE 17).  kPass2Add (tests only: the kernel xors the bias away):
-// rounding constant minus 32768 * row sum
-// (the u16 row image carries +32768).
+// DESCALE 4; others: DESCALE 17).
 #define MJG_PASS2_DOT                                                  \
   {1, 1, 1, 1, 1, 1, 1, 1,                                             \
    11363, 9633, 6437, 2260, -2260, -6437, -9633, -11363,               \
@@ -58,7 +59,10 @@ constexpr float kRnd = 0x1p-10f;
 __device__ static constexpr int kPass2Dot[64] = MJG_PASS2_DOT;
 // The kernel's pass-2 rows (s_m2): rows 0 and 4 scaled by 2^13, so every row is accumulated
 // from 2^16 and descaled by 17 (2^13 (S + 8) >> 17 == (S + 8) >> 4; |S| <= 8 * 32640, so
-// 2^13 (S + 8) stays below 2^31): no per-row start value or shift in exact_coef.
+// 2^13 (S + 8) stays below 2^31): no per-row shift in exact_coef.  The image's +16384 of
+// columns 1-7 cancels in every row but row 0 (its entries sum to 2^16), where the start value
+// is 2^16 - 2^30 instead (kRow0Bias, carried in the descriptor's top bits).
+constexpr uint32_t kRow0Bias = 0xC0000000u;  // -2^30 = -16384 * 2^16
 constexpr int kPass2DcScale = 8192;
 __device__ __forceinline__ uint32_t pass2_pair(int i) {  // int16 pair of entries 2i, 2i + 1
   const int r = i >> 2, f = (r & 3) == 0 ? kPass2DcScale : 1;
@@ -72,8 +76,6 @@ __device__ static constexpr uint8_t kScreenScatter[64] = {
     36, 34, 22, 19, 11, 8, 4, 1, 35, 21, 20, 10, 9, 3, 2, 0,
     63, 61, 60, 54, 53, 43, 42, 28, 62, 59, 55, 52, 44, 41, 29, 27,
     58, 56, 51, 45, 40, 30, 26, 15, 57, 50, 46, 39, 31, 25, 16, 14};
-__device__ static constexpr int kPass2Add[8] = {8 - 8 * 32768, 1 << 16, 1 << 16, 1 << 16,
-                                                8, 1 << 16, 1 << 16, 1 << 16};
 
 // Frame geometry.  A frame is a raster of MCUs of `bpm` blocks each (4:2:0: 16x16, Y0-3 Cb
 // Cr; 4:2:2: 16x16, Y0-3 Cb0 Cb1 Cr0 Cr1; 4:4:4: 8x16, Y0 Y1 Cb0 Cb1 Cr0 Cr1 -- FFmpeg's
@@ -285,12 +287,12 @@ struct ShiftSink {
 constexpr int kStageWords = (kMaxBlockBits + 31) / 32;  // staged words per lane
 
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
-// image (pkcol = s_pk + lane: word [r*4 + c/2] holds rows r, columns c, c+1 as u16 = value
-// + 32768).  jfdctint pass 2 for output row ro is one integer dot product over the column
-// (the LLM butterfly's products and sums folded into kPass2Dot[ro][*]): v_perm gathers the
-// column's rows r, r+1 into one word, the xor with 0x8000 per half turns value + 32768 into
-// the signed value, and v_dot2_i32_i16 multiplies two rows at a time against the packed
-// coefficient pairs m2p[ro][*] (exact: every product and sum fits int32).  Then DESCALE and
+// image (pkcol = s_pk + lane: word [r*4 + c/2] holds rows r, columns c, c+1 as u16 = value,
+// + 16384 for columns 1-7).  jfdctint pass 2 for output row ro is one integer dot product over
+// the column (the LLM butterfly's products and sums folded into kPass2Dot[ro][*]): v_perm
+// gathers the column's rows r, r+1 into one word and v_dot2_i32_i16 multiplies two rows at a
+// time against the packed coefficient pairs m2p[ro][*] (pass2_pair; every u16 is below 2^15,
+// so int16 reads it unchanged, and the bias cancels or is started out, see kRow0Bias).  Then DESCALE and
 // dct_quantize_c's intra rounding: sign(u) * ((|u| * qmat + 3<<18) >> 21), folded into one
 // signed multiply-add.
 typedef short short2_t __attribute__((ext_vector_type(2)));
@@ -300,11 +302,11 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
   const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
   const uint4 mp = *(const uint4 *)(m2p + ro * 4);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  int acc = 1 << 16;  // rows 0 / 4 scaled (pass2_pair)
+  int acc = (int)((ro == 0 && c != 0 ? kRow0Bias : 0u) | 0x10000u);  // see pass2_pair
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t w0 = pkcol[((2 * i) * 4 + (c >> 1)) * 64], w1 = pkcol[((2 * i + 1) * 4 + (c >> 1)) * 64];
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel) ^ 0x80008000u;
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel);
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
                                  false);
   }
@@ -314,24 +316,26 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
 }
 
 // exact_coef for zigzag position k from its descriptor (zz_desc, in LDS), returned as
-// t = v - (v < 0) (see emit_ac): x = the v_perm selector of the column's u16 half, y = qmat,
-// z = the pass-2 row's byte offset in s_m2, w = the column pair's byte offset in the row
-// image.  One 16-byte LDS read per candidate replaces the zigzag, qmat and row tables and
-// every field extraction.
+// t = v - (v < 0) (see emit_ac): x = the v_perm selector of the column's u16 half, y = qmat
+// (bits 0-17; v_mul_i32_i24 ignores bits 24-31) | kRow0Bias for row 0, columns 1-7 (the
+// accumulator's start value is y & kRow0Bias | 2^16), z = the pass-2 row's byte offset in s_m2,
+// w = the column pair's byte offset in the row image.  One 16-byte LDS read per candidate
+// replaces the zigzag, qmat and row tables and every field extraction.
 __device__ __forceinline__ uint4 zz_desc(int k, const uint32_t *tabs) {
   const int n = kZigzag[k], ro = n >> 3, c = n & 7;
-  return make_uint4((c & 1) ? 0x07060302u : 0x05040100u, tabs[544 + c * 8 + ro], (uint32_t)ro * 16u,
+  return make_uint4((c & 1) ? 0x07060302u : 0x05040100u,
+                    tabs[544 + c * 8 + ro] | (ro == 0 && c != 0 ? kRow0Bias : 0u), (uint32_t)ro * 16u,
                     (uint32_t)(c >> 1) * 256u);
 }
 __device__ __forceinline__ int exact_coef_t(const uint32_t *pkcol, uint4 d, const uint32_t *m2p) {
   const uint32_t *col = (const uint32_t *)((const uint8_t *)pkcol + d.w);
   const uint4 mp = *(const uint4 *)((const uint8_t *)m2p + d.z);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  int acc = 1 << 16;
+  int acc = (int)((d.y & kRow0Bias) | 0x10000u);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t w0 = col[((2 * i) * 4) * 64], w1 = col[((2 * i + 1) * 4) * 64];
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x) ^ 0x80008000u;
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x);
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
                                  false);
   }
@@ -408,12 +412,12 @@ __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, in
   const uint32_t cc = d.w >> 8;  // column pair
   const uint4 mp = *(const uint4 *)((const uint8_t *)m2 + d.z);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  int acc = 1 << 16;
+  int acc = (int)((d.y & kRow0Bias) | 0x10000u);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i) * 4 + cc) << 2), (int)wv);
     const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i + 1) * 4 + cc) << 2), (int)wv);
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x) ^ 0x80008000u;
+    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x);
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc, false);
   }
   const int u = acc >> 17;
@@ -759,14 +763,15 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
 }
 
 // Row pass of one chunk, lane = block: raw rows (8 little-endian words of 8 pixels) ->
-// the wave's LDS row image s_pk ([word][lane], u16 pairs of value + 32768).
+// the wave's LDS row image s_pk ([word][lane], u16 pairs; output 0 as is, 1-7 + 16384).
 template <bool RC>
 __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, const uint8_t *s_rc,
                                          uint32_t *s_pk, int lane) {
   // Row pass (jfdctint pass 1) in fp32, exactly: every value is an integer or a multiple
   // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
   // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
-  // (M' = 1.5*2^23 + 32768), which also leaves x + 32768 in the low 16 mantissa bits:
+  // (M' = kMc = 1.5*2^23 + 16384; kM for output 0), which also leaves x + 16384 (x) in the
+  // low 16 mantissa bits:
   // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
   // [RC] swscale tv->pc per pixel from a 512-byte LDS table (clip_u8((p * A21 - B21) >> 21),
   // checked exhaustively in tests/test_oracle.py), OR'ed into the mantissa of M = 1.5*2^23:
@@ -807,18 +812,18 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
     const float t7 = p[0] - p[7], t6 = p[1] - p[6], t5 = p[2] - p[5], t4 = p[3] - p[4];
     const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
     float o[8];
-    o[0] = __builtin_fmaf(t10 + t11, 16.0f, kMb);
-    o[4] = __builtin_fmaf(t10 - t11, 16.0f, kMb);
-    o[2] = __builtin_fmaf(t13, 10703.0f / 512, __builtin_fmaf(t12, 4433.0f / 512, kRnd)) + kMb;
-    o[6] = __builtin_fmaf(t13, 4433.0f / 512, __builtin_fmaf(t12, -10704.0f / 512, kRnd)) + kMb;
+    o[0] = __builtin_fmaf(t10 + t11, 16.0f, kM);  // the row sum: unbiased (0..32640)
+    o[4] = __builtin_fmaf(t10 - t11, 16.0f, kMc);
+    o[2] = __builtin_fmaf(t13, 10703.0f / 512, __builtin_fmaf(t12, 4433.0f / 512, kRnd)) + kMc;
+    o[6] = __builtin_fmaf(t13, 4433.0f / 512, __builtin_fmaf(t12, -10704.0f / 512, kRnd)) + kMc;
     o[1] = __builtin_fmaf(t7, 11363.0f / 512, __builtin_fmaf(t6, 9633.0f / 512,
-           __builtin_fmaf(t5, 6437.0f / 512, __builtin_fmaf(t4, 2260.0f / 512, kRnd)))) + kMb;
+           __builtin_fmaf(t5, 6437.0f / 512, __builtin_fmaf(t4, 2260.0f / 512, kRnd)))) + kMc;
     o[3] = __builtin_fmaf(t7, 9633.0f / 512, __builtin_fmaf(t6, -2259.0f / 512,
-           __builtin_fmaf(t5, -11362.0f / 512, __builtin_fmaf(t4, -6436.0f / 512, kRnd)))) + kMb;
+           __builtin_fmaf(t5, -11362.0f / 512, __builtin_fmaf(t4, -6436.0f / 512, kRnd)))) + kMc;
     o[5] = __builtin_fmaf(t7, 6437.0f / 512, __builtin_fmaf(t6, -11362.0f / 512,
-           __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMb;
+           __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMc;
     o[7] = __builtin_fmaf(t7, 2260.0f / 512, __builtin_fmaf(t6, -6436.0f / 512,
-           __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMb;
+           __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMc;
 #pragma unroll
     for (int j = 0; j < 4; j++)
       s_pk[(r * 4 + j) * 64 + lane] =
@@ -849,7 +854,7 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
     // column's row-pass values are small enough.  Rows 1-7 of pass 2 have coefficient
     // sums 0, so |S_k| <= L1(row k) * R / 2 with R = max - min of the column; row 0 is
     // the plain sum, |S_0| <= 8 max|u|.  open_ctx turns the quantiser thresholds into
-    // limits on R, max and min (u16 with the +32768 bias), tested with packed u16
+    // limits on R, max and min (u16 with the +16384 bias), tested with packed u16
     // max/min and saturating subtracts; a column is skipped when every block of the
     // chunk passes (wave ballot), its 8 screen bits are then 0.
     bool skip0 = false, skip1 = false;
@@ -884,11 +889,13 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
 #pragma unroll
       for (int r = 0; r < 8; r++)
         x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));
-      // x = M' + value: differences cancel the bias, sums drop it with one -2M'
-      const float t0 = (x[0] - 2.0f * kMb) + x[7], t7 = x[0] - x[7];
-      const float t1 = (x[1] - 2.0f * kMb) + x[6], t6 = x[1] - x[6];
-      const float t2 = (x[2] - 2.0f * kMb) + x[5], t5 = x[2] - x[5];
-      const float t3 = (x[3] - 2.0f * kMb) + x[4], t4 = x[3] - x[4];
+      // x = M' + value (M' = kM for column 0, kMc for the others): differences cancel the
+      // bias, sums drop it with one -2M'
+      const float kB2 = col == 0 ? 2.0f * kM : 2.0f * kMc;
+      const float t0 = (x[0] - kB2) + x[7], t7 = x[0] - x[7];
+      const float t1 = (x[1] - kB2) + x[6], t6 = x[1] - x[6];
+      const float t2 = (x[2] - kB2) + x[5], t5 = x[2] - x[5];
+      const float t3 = (x[3] - kB2) + x[4], t4 = x[3] - x[4];
       const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
       float sv[8];
       sv[0] = t10 + t11;
@@ -958,9 +965,10 @@ __device__ __forceinline__ int dc_predictor(int dc, int carry, int delta, bool f
 //     FFmpeg descales by 9 (a power of two: still exact).  Every partial sum is a multiple of
 //     2^-10 below 2^14 (|sum| <= 128 * 59642 / 512), so the f32 accumulation is exact in any
 //     order; the accumulator starts at 2^-10 (0 for outputs 0/4), so adding M' = 1.5 2^23 +
-//     32768 rounds to FFmpeg's DESCALE and leaves y + 32768 in the low mantissa bits, the u16
+//     16384 rounds to FFmpeg's DESCALE and leaves y + 16384 in the low mantissa bits, the u16
 //     row image s_pk of the VALU row pass.  Centring moves only the row sums (output 0) by a
-//     constant, which every AC row of pass 2 cancels (its coefficients sum to 0).
+//     constant, which every AC row of pass 2 cancels (its coefficients sum to 0); centred,
+//     they too fit 0..32767 with the +16384 (exact_coef never reads column 0's row 0).
 //   pass 2, a screen: Z_t[z][blk] = sum_k A2[z][k] * f16(D)[k][blk] with A2 = pass-2 rows
 //     scaled by 2^10 / tau_z, tau_z = the quantiser threshold of zigzag coefficient z minus
 //     the f16 rounding bound (open_ctx): |Z| > 2^10 whenever the coefficient quantises to
@@ -1047,7 +1055,8 @@ __device__ __forceinline__ uint32_t dct_group(const uint32_t (&rows)[4][2], int 
   for (int t = 0; t < 2; t++) {
 #pragma unroll
     for (int q = 0; q < 16; q += 2) {
-      const uint32_t o0 = __float_as_uint(d[t][q] + kMb), o1 = __float_as_uint(d[t][q + 1] + kMb);
+      // + 16384 on every output: the centred row sums (-16384..16256) included
+      const uint32_t o0 = __float_as_uint(d[t][q] + kMc), o1 = __float_as_uint(d[t][q + 1] + kMc);
       pk[((4 * t + (q >> 2)) * 4 + ((q & 3) >> 1)) * 64] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);
     }
 #pragma unroll

@@ -22,7 +22,8 @@ import oracle
 SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "ffmpeg_distributed_amd", "csrc", "kernels.hip")
 M = np.float32(12582912.0)
-MB = np.float32(12615680.0)
+MC = np.float32(12599296.0)  # kMc = kM + 16384
+BIAS = np.array([0] + [16384] * 7, np.int64)  # the row image's bias per row-pass output
 RND = np.float32(2.0 ** -10)
 
 
@@ -99,7 +100,7 @@ def pass1_int(p):
 
 
 def pass1_f32(p, rc_chroma=None):
-    """The kernel's fp32 row pass; returns the u16 image values (value + 32768)."""
+    """The kernel's fp32 row pass; returns the u16 image values (value + BIAS[output])."""
     f = lambda a: np.asarray(a, np.float32)
     if rc_chroma is None:
         x = [f(p[:, i]) for i in range(8)]
@@ -114,10 +115,10 @@ def pass1_f32(p, rc_chroma=None):
     t10, t13, t11, t12 = f(t0 + t3), f(t0 - t3), f(t1 + t2), f(t1 - t2)
     c = lambda v: np.float32(v / 512)
     o = [None] * 8
-    o[0] = fma32(f(t10 + t11), 16.0, MB)
-    o[4] = fma32(f(t10 - t11), 16.0, MB)
-    o[2] = f(fma32(t13, c(10703), fma32(t12, c(4433), RND)) + MB)
-    o[6] = f(fma32(t13, c(4433), fma32(t12, c(-10704), RND)) + MB)
+    o[0] = fma32(f(t10 + t11), 16.0, M)
+    o[4] = fma32(f(t10 - t11), 16.0, MC)
+    o[2] = f(fma32(t13, c(10703), fma32(t12, c(4433), RND)) + MC)
+    o[6] = f(fma32(t13, c(4433), fma32(t12, c(-10704), RND)) + MC)
     odd = {1: (2260, 6437, 9633, 11363), 3: (-6436, -11362, -2259, 9633),
            5: (9633, 2261, -11362, 6437), 7: (-11363, 9633, -6436, 2260)}
     for k, (c4, c5, c6, c7) in odd.items():
@@ -125,7 +126,7 @@ def pass1_f32(p, rc_chroma=None):
         a = fma32(t5, c(c5), a)
         a = fma32(t6, c(c6), a)
         a = fma32(t7, c(c7), a)
-        o[k] = f(a + MB)
+        o[k] = f(a + MC)
     bits = np.stack([v.view(np.uint32) for v in o], 1)
     return (bits & 0xFFFF).astype(np.int64)
 
@@ -140,7 +141,9 @@ def _rows(rng, n):
 def test_fp32_row_pass_equals_jfdctint_pass1():
     rng = np.random.default_rng(1)
     p = _rows(rng, 200000)
-    assert (pass1_f32(p) - 32768 == pass1_int(p)).all()
+    img = pass1_f32(p)
+    assert (img - BIAS == pass1_int(p)).all()
+    assert ((img >= 0) & (img < 32768)).all()  # reads as the same value in int16 (exact_coef)
 
 
 @pytest.mark.parametrize("chroma", [False, True])
@@ -148,18 +151,18 @@ def test_fp32_row_pass_with_range_convert(chroma):
     rng = np.random.default_rng(2 + chroma)
     p = _rows(rng, 100000)
     ref = pass1_int(range_int(p.astype(np.int64), chroma))
-    assert (pass1_f32(p, rc_chroma=chroma) - 32768 == ref).all()
+    assert (pass1_f32(p, rc_chroma=chroma) - BIAS == ref).all()
 
 
 def test_pass2_dot_rows_equal_oracle_fdct():
     dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
-    add = np.array(_int_array("kPass2Add"), np.int64)
+    add = np.array([8, 1 << 16, 1 << 16, 1 << 16, 8, 1 << 16, 1 << 16, 1 << 16], np.int64)
     sh = np.array([4, 17, 17, 17, 4, 17, 17, 17])
     rng = np.random.default_rng(3)
     for it in range(300):
         blk = rng.integers(0, 256, (8, 8)) if it % 3 else rng.choice([0, 255], (8, 8))
         ref = oracle.fdct(blk.astype(np.int16)).reshape(8, 8).astype(np.int64)
-        img = pass1_f32(blk)  # rows -> u16 image (value + 32768), [row][col]
+        img = pass1_f32(blk) - BIAS  # rows -> row-pass values, [row][col]
         for c in range(8):
             col = img[:, c]
             acc = (dot @ col + add).astype(np.int64)
@@ -168,19 +171,28 @@ def test_pass2_dot_rows_equal_oracle_fdct():
 
 
 def test_pass2_scaled_dc_rows_equal_oracle_fdct():
-    """k_encode's s_m2 (pass2_pair): rows 0 and 4 scaled by kPass2DcScale, every row started
-    at 2^16 and descaled by 17, on signed row-pass values; int32 never wraps (extreme blocks)."""
+    """exact_coef as k_encode runs it: s_m2 rows 0 and 4 scaled by kPass2DcScale, the biased
+    u16 image read as int16, the accumulator started at 2^16 (2^16 + kRow0Bias for row 0,
+    columns 1-7), int32 wraparound, descaled by 17 -- equal to the oracle FDCT, and the true
+    accumulator never leaves int32 (extreme blocks)."""
     scale = int(re.search(r"constexpr int kPass2DcScale = (\d+);", _src()).group(1))
+    row0 = int(re.search(r"constexpr uint32_t kRow0Bias = (0x[0-9A-Fa-f]+)u;", _src()).group(1), 16)
+    row0 -= 1 << 32
     dot = np.array(_int_array("kPass2Dot"), np.int64).reshape(8, 8)
     dot[[0, 4]] *= scale
+    start = np.full((8, 8), 1 << 16, np.int64)
+    start[0, 1:] += row0
     rng = np.random.default_rng(5)
     blocks = [np.full((8, 8), 255), np.zeros((8, 8), np.int64)]
     blocks += [rng.choice([0, 255], (8, 8)) for _ in range(100)] + [rng.integers(0, 256, (8, 8)) for _ in range(200)]
     for blk in blocks:
         ref = oracle.fdct(blk.astype(np.int16)).reshape(8, 8).astype(np.int64)
-        img = pass1_f32(blk) - 32768
-        acc = dot @ img + (1 << 16)
-        assert (np.abs(acc) < 2 ** 31).all()
+        img = pass1_f32(blk)
+        true = dot @ (img - BIAS) + (1 << 16)
+        assert (np.abs(true) < 2 ** 31).all()
+        acc = dot @ img + start
+        acc = ((acc + 2 ** 31) % 2 ** 32) - 2 ** 31  # int32 wraparound, as on the GPU
+        assert (acc == true).all()
         assert ((acc >> 17) == ref).all()
 
 
@@ -197,7 +209,7 @@ def test_screen_thresholds_are_conservative():
             img = pass1_f32(blk)
             coefs = oracle.quantize(oracle.fdct(blk.astype(np.int16)), q)[0].reshape(8, 8)
             for c in range(8):
-                s_exact = dot @ (img[:, c] - 32768)
+                s_exact = dot @ (img[:, c] - BIAS[c])
                 for r in range(8):
                     n = r * 8 + c
                     if n == 0 or coefs[r, c] == 0:
