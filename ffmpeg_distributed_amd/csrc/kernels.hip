@@ -287,58 +287,48 @@ struct ShiftSink {
 constexpr int kStageWords = (kMaxBlockBits + 31) / 32;  // staged words per lane
 
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
-// image (pkcol = s_pk + lane: word [r*4 + c/2] holds rows r, columns c, c+1 as u16 = value,
-// + 16384 for columns 1-7).  jfdctint pass 2 for output row ro is one integer dot product over
-// the column (the LLM butterfly's products and sums folded into kPass2Dot[ro][*]): v_perm
-// gathers the column's rows r, r+1 into one word and v_dot2_i32_i16 multiplies two rows at a
-// time against the packed coefficient pairs m2p[ro][*] (pass2_pair; every u16 is below 2^15,
-// so int16 reads it unchanged, and the bias cancels or is started out, see kRow0Bias).  Then DESCALE and
-// dct_quantize_c's intra rounding: sign(u) * ((|u| * qmat + 3<<18) >> 21), folded into one
-// signed multiply-add.
+// image (pkcol = s_pk + lane: word [c*4 + r/2] holds column c of rows r, r+1 (r even) as u16
+// = value, + 16384 for columns 1-7).  jfdctint pass 2 for output row ro is one integer dot
+// product over the column (the LLM butterfly's products and sums folded into kPass2Dot[ro][*]):
+// v_dot2_i32_i16 multiplies a word (two rows) at a time against the packed coefficient pairs
+// m2p[ro][*] (pass2_pair; every u16 is below 2^15, so int16 reads it unchanged, and the bias
+// cancels or is started out, see kRow0Bias).  Then DESCALE and dct_quantize_c's intra
+// rounding: sign(u) * ((|u| * qmat + 3<<18) >> 21), folded into one signed multiply-add.
 typedef short short2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const uint32_t *m2p,
                                           const int *qc) {
   const int ro = n >> 3, c = n & 7;
-  const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
   const uint4 mp = *(const uint4 *)(m2p + ro * 4);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
   int acc = (int)((ro == 0 && c != 0 ? kRow0Bias : 0u) | 0x10000u);  // see pass2_pair
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t w0 = pkcol[((2 * i) * 4 + (c >> 1)) * 64], w1 = pkcol[((2 * i + 1) * 4 + (c >> 1)) * 64];
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel);
-    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
-                                 false);
-  }
+  for (int i = 0; i < 4; i++)
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pkcol[(c * 4 + i) * 64]),
+                                 __builtin_bit_cast(short2_t, m[i]), acc, false);
   const int u = acc >> 17;
   const int qm = qc[c * 8 + ro];
   return (__mul24(u, qm) + (u < 0 ? (1 << 21) - 1 - (3 << 18) : (3 << 18))) >> 21;
 }
 
 // exact_coef for zigzag position k from its descriptor (zz_desc, in LDS), returned as
-// t = v - (v < 0) (see emit_ac): x = the v_perm selector of the column's u16 half, y = qmat
-// (bits 0-17; v_mul_i32_i24 ignores bits 24-31) | kRow0Bias for row 0, columns 1-7 (the
-// accumulator's start value is y & kRow0Bias | 2^16), z = the pass-2 row's byte offset in s_m2,
-// w = the column pair's byte offset in the row image.  One 16-byte LDS read per candidate
-// replaces the zigzag, qmat and row tables and every field extraction.
+// t = v - (v < 0) (see emit_ac): x = the accumulator's start value (2^16, plus kRow0Bias for
+// row 0, columns 1-7), y = qmat, z = the pass-2 row's byte offset in s_m2, w = the column's
+// byte offset in the row image.  One 16-byte LDS read per candidate replaces the zigzag, qmat
+// and row tables and every field extraction.
 __device__ __forceinline__ uint4 zz_desc(int k, const uint32_t *tabs) {
   const int n = kZigzag[k], ro = n >> 3, c = n & 7;
-  return make_uint4((c & 1) ? 0x07060302u : 0x05040100u,
-                    tabs[544 + c * 8 + ro] | (ro == 0 && c != 0 ? kRow0Bias : 0u), (uint32_t)ro * 16u,
-                    (uint32_t)(c >> 1) * 256u);
+  return make_uint4((ro == 0 && c != 0 ? kRow0Bias : 0u) | 0x10000u, tabs[544 + c * 8 + ro],
+                    (uint32_t)ro * 16u, (uint32_t)c * 4u * 64u * 4u);
 }
 __device__ __forceinline__ int exact_coef_t(const uint32_t *pkcol, uint4 d, const uint32_t *m2p) {
   const uint32_t *col = (const uint32_t *)((const uint8_t *)pkcol + d.w);
   const uint4 mp = *(const uint4 *)((const uint8_t *)m2p + d.z);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  int acc = (int)((d.y & kRow0Bias) | 0x10000u);
+  int acc = (int)d.x;
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t w0 = col[((2 * i) * 4) * 64], w1 = col[((2 * i + 1) * 4) * 64];
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x);
-    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc,
-                                 false);
-  }
+  for (int i = 0; i < 4; i++)
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, col[i * 64]), __builtin_bit_cast(short2_t, m[i]),
+                                 acc, false);
   const int u = acc >> 17;
   // t = v - (v < 0) (mag_cat's t) directly: for u < 0 the rounding constant less 2^21
   return (__mul24(u, (int)d.y) + (u < 0 ? -1 - (3 << 18) : (3 << 18))) >> 21;
@@ -409,15 +399,13 @@ __device__ __noinline__ uint32_t emit_block_wave(const uint32_t *s_pk, int h, in
                                                  uint32_t *stage_w, int lane) {
   const uint32_t wv = lane < 32 ? s_pk[lane * 64 + h] : 0u;
   const uint4 d = zd[lane];
-  const uint32_t cc = d.w >> 8;  // column pair
+  const uint32_t cw = d.w >> 6;  // byte offset of the column's first word in wv's lanes (4 * c * 4)
   const uint4 mp = *(const uint4 *)((const uint8_t *)m2 + d.z);
   const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
-  int acc = (int)((d.y & kRow0Bias) | 0x10000u);
+  int acc = (int)d.x;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i) * 4 + cc) << 2), (int)wv);
-    const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((((2 * i + 1) * 4 + cc) << 2), (int)wv);
-    const uint32_t pr = __builtin_amdgcn_perm(w1, w0, d.x);
+    const uint32_t pr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)cw + 4 * i, (int)wv);
     acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc, false);
   }
   const int u = acc >> 17;
@@ -763,7 +751,8 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
 }
 
 // Row pass of one chunk, lane = block: raw rows (8 little-endian words of 8 pixels) ->
-// the wave's LDS row image s_pk ([word][lane], u16 pairs; output 0 as is, 1-7 + 16384).
+// the wave's LDS row image s_pk ([word][lane]; word c*4 + r/2 = column c of rows r, r+1 as
+// u16 pairs; output 0 as is, 1-7 + 16384).
 template <bool RC>
 __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, const uint8_t *s_rc,
                                          uint32_t *s_pk, int lane) {
@@ -771,14 +760,13 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
   // of 2^-10 below 2^14 (24 significant bits), each fma rounds nothing, and the DESCALE
   // floor((x + 256) / 512) is the single round-to-nearest-even of (x/512 + 2^-10) + M'
   // (M' = kMc = 1.5*2^23 + 16384; kM for output 0), which also leaves x + 16384 (x) in the
-  // low 16 mantissa bits:
-  // one v_perm packs two outputs as u16 pairs into the wave's LDS row image.
+  // low 16 mantissa bits: one v_perm packs an output of two rows as a u16 pair into the
+  // wave's LDS row image (rows in pairs: exact_coef then reads two rows of a column per word).
   // [RC] swscale tv->pc per pixel from a 512-byte LDS table (clip_u8((p * A21 - B21) >> 21),
   // checked exhaustively in tests/test_oracle.py), OR'ed into the mantissa of M = 1.5*2^23:
   // values then carry the +M bias, which the butterfly's differences cancel and its sums
   // remove with one -2M.
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
+  auto row = [&](int r, float (&o)[8]) {
     const uint32_t lo = (uint32_t)raw[r], hi = (uint32_t)(raw[r] >> 32);
     float p[8];
     p[0] = (float)((lo >> 0) & 255u);  // v_cvt_f32_ubyte0
@@ -811,7 +799,6 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
     }
     const float t7 = p[0] - p[7], t6 = p[1] - p[6], t5 = p[2] - p[5], t4 = p[3] - p[4];
     const float t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
-    float o[8];
     o[0] = __builtin_fmaf(t10 + t11, 16.0f, kM);  // the row sum: unbiased (0..32640)
     o[4] = __builtin_fmaf(t10 - t11, 16.0f, kMc);
     o[2] = __builtin_fmaf(t13, 10703.0f / 512, __builtin_fmaf(t12, 4433.0f / 512, kRnd)) + kMc;
@@ -824,14 +811,20 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
            __builtin_fmaf(t5, 2261.0f / 512, __builtin_fmaf(t4, 9633.0f / 512, kRnd)))) + kMc;
     o[7] = __builtin_fmaf(t7, 2260.0f / 512, __builtin_fmaf(t6, -6436.0f / 512,
            __builtin_fmaf(t5, 9633.0f / 512, __builtin_fmaf(t4, -11363.0f / 512, kRnd)))) + kMc;
+  };
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      s_pk[(r * 4 + j) * 64 + lane] =
-          __builtin_amdgcn_perm(__float_as_uint(o[2 * j + 1]), __float_as_uint(o[2 * j]), 0x05040100u);
+  for (int rp = 0; rp < 4; rp++) {
+    float a[8], b[8];
+    row(2 * rp, a);
+    row(2 * rp + 1, b);
+#pragma unroll
+    for (int c = 0; c < 8; c++)
+      s_pk[(c * 4 + rp) * 64 + lane] = __builtin_amdgcn_perm(__float_as_uint(b[c]), __float_as_uint(a[c]), 0x05040100u);
 #ifndef MJG_EXP_NO_SB_ROW
     __builtin_amdgcn_sched_barrier(0);
 #endif
-  }}
+  }
+}
 
   // Column pass (jfdctint pass 2) as a float *screen*: the products of pass 2 need up to
   // 31 bits, so fp32 sums are only approximate (|error| < 2^9 before the 2^17 descale).
@@ -847,9 +840,9 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
 #ifndef MJG_EXP_NO_SB_PAIR
     __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
 #endif
-    uint32_t w[8];
+    uint32_t w[8];  // w[4h + i]: column 2jp + h of rows 2i (low half), 2i + 1 (high half)
 #pragma unroll
-    for (int r = 0; r < 8; r++) w[r] = s_pk[(r * 4 + jp) * 64 + lane];
+    for (int i = 0; i < 8; i++) w[i] = s_pk[(jp * 8 + i) * 64 + lane];
     // Column skip (pairs 1-3): every AC output of a column quantises to zero when the
     // column's row-pass values are small enough.  Rows 1-7 of pass 2 have coefficient
     // sums 0, so |S_k| <= L1(row k) * R / 2 with R = max - min of the column; row 0 is
@@ -859,12 +852,19 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
     // chunk passes (wave ballot), its 8 screen bits are then 0.
     bool skip0 = false, skip1 = false;
     if (jp > 0) {
-      u16x2 mx = as_u16x2(w[0]), mn = mx;
+      u16x2 ma = as_u16x2(w[0]), na = ma, mb = as_u16x2(w[4]), nb = mb;
 #pragma unroll
-      for (int r = 1; r < 8; r++) {
-        mx = __builtin_elementwise_max(mx, as_u16x2(w[r]));
-        mn = __builtin_elementwise_min(mn, as_u16x2(w[r]));
+      for (int i = 1; i < 4; i++) {
+        ma = __builtin_elementwise_max(ma, as_u16x2(w[i]));
+        na = __builtin_elementwise_min(na, as_u16x2(w[i]));
+        mb = __builtin_elementwise_max(mb, as_u16x2(w[4 + i]));
+        nb = __builtin_elementwise_min(nb, as_u16x2(w[4 + i]));
       }
+      // (column 2jp, column 2jp + 1): each column's even-row and odd-row halves combined
+      const u16x2 mx = __builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(as_u32(mb), as_u32(ma), 0x05040100u)),
+                                                 as_u16x2(__builtin_amdgcn_perm(as_u32(mb), as_u32(ma), 0x07060302u)));
+      const u16x2 mn = __builtin_elementwise_min(as_u16x2(__builtin_amdgcn_perm(as_u32(nb), as_u32(na), 0x05040100u)),
+                                                 as_u16x2(__builtin_amdgcn_perm(as_u32(nb), as_u32(na), 0x07060302u)));
       const uint32_t t =
           as_u32(__builtin_elementwise_sub_sat(mx - mn, as_u16x2(s_skip[3 * jp - 3]))) |
           as_u32(__builtin_elementwise_sub_sat(mx, as_u16x2(s_skip[3 * jp - 2]))) |
@@ -888,7 +888,7 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
       float x[8];
 #pragma unroll
       for (int r = 0; r < 8; r++)
-        x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[r], h ? 0x07060302u : 0x07060100u));
+        x[r] = __uint_as_float(__builtin_amdgcn_perm(0x4B400000u, w[4 * h + r / 2], (r & 1) ? 0x07060302u : 0x07060100u));
       // x = M' + value (M' = kM for column 0, kMc for the others): differences cancel the
       // bias, sums drop it with one -2M'
       const float kB2 = col == 0 ? 2.0f * kM : 2.0f * kMc;
@@ -1047,17 +1047,17 @@ __device__ __forceinline__ uint32_t dct_group(const uint32_t (&rows)[4][2], int 
     d[t] = mfma16(p1h, bp[2 * t + 1], d[t]);
     d[t] = mfma16(p1l, bp[2 * t + 1], d[t]);
   }
-  // s_pk: word (r * 4 + i / 2) of block 32g + (lane & 31); this lane holds outputs
-  // i = 4h .. 4h+3 of rows 4t .. 4t+3
-  uint32_t *pk = s_pk + (lane >> 5) * 2 * 64 + g * 32 + (lane & 31);
+  // s_pk: word (i * 4 + r / 2) of block 32g + (lane & 31); this lane holds outputs
+  // i = 4h .. 4h+3 of rows 4t .. 4t+3 (register q: row 4t + q / 4, output 4h + q % 4)
+  uint32_t *pk = s_pk + (lane >> 5) * 16 * 64 + g * 32 + (lane & 31);
   uint4 b2[4];
 #pragma unroll
   for (int t = 0; t < 2; t++) {
 #pragma unroll
-    for (int q = 0; q < 16; q += 2) {
+    for (int q = 0; q < 16; q = (q & 3) == 3 ? q + 5 : q + 1) {  // q = 0-3, 8-11: rows 4t + 2 (q >> 3), + 1
       // + 16384 on every output: the centred row sums (-16384..16256) included
-      const uint32_t o0 = __float_as_uint(d[t][q] + kMc), o1 = __float_as_uint(d[t][q + 1] + kMc);
-      pk[((4 * t + (q >> 2)) * 4 + ((q & 3) >> 1)) * 64] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);
+      const uint32_t o0 = __float_as_uint(d[t][q] + kMc), o1 = __float_as_uint(d[t][q + 4] + kMc);
+      pk[((q & 3) * 4 + 2 * t + (q >> 3)) * 64] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);
     }
 #pragma unroll
     for (int s = 0; s < 2; s++) {
