@@ -11,6 +11,7 @@ build are wrong by construction; only kernel times (and SQ counters) are compare
   noexact  : exact_coef returns a constant (the candidate loop and coding kept)
   noscreen : column screen skipped (DC from the row image, no candidates): loads + row pass +
              DC/EOB coding + pack
+  nohbm    : every chunk reads frame 0 or 1 (Infinity-Cache resident): memory's share
   nodct    : row pass and column screen skipped (raw rows copied into the LDS image): loads +
              LDS image + DC/EOB coding + pack
 
@@ -32,7 +33,11 @@ EXACT = "  const uint32_t *col = pkcol + ((d.y >> 18) & 3u) * 64;\n"
 SCREEN = "      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);"
 ROWPASS = "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);"
 
+FBASE = "  auto frame_base = [&](int f) { return frames + (size_t)f * g.frame_stride; };"
+
 SUBS = {
+    # every chunk reads frame 0 or 1 (25 MB: Infinity-Cache resident): the memory system's share
+    "nohbm": [(FBASE, "  auto frame_base = [&](int f) { return frames + (size_t)(f & 1) * g.frame_stride; };")],
     "noemit": [(EMIT, "      q.emit(((uint32_t)__popcll(mask) << 8) ^ ((uint32_t)diff & 255u), 16);\n"
                       "      q.finish();\n"),
                (WIDE, "const uint64_t wide = 0;")],
