@@ -480,7 +480,10 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
   int best_cost = serial;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const int cost = 4 * __popcll(hv[k]) + (4 << k);
+#ifndef MJG_EXP_WIDE_COST
+#define MJG_EXP_WIDE_COST 4
+#endif
+    const int cost = MJG_EXP_WIDE_COST * __popcll(hv[k]) + (4 << k);
     if (hv[k] && cost < best_cost) {
       best_cost = cost;
       best = hv[k];
