@@ -854,7 +854,11 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
     // max/min and saturating subtracts; a column is skipped when every block of the
     // chunk passes (wave ballot), its 8 screen bits are then 0.
     bool skip0 = false, skip1 = false;
+#ifdef MJG_EXP_NO_SKIP
+    if (false) {
+#else
     if (jp > 0) {
+#endif
       u16x2 ma = as_u16x2(w[0]), na = ma, mb = as_u16x2(w[4]), nb = mb;
 #pragma unroll
       for (int i = 1; i < 4; i++) {
