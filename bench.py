@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=4.0,
                    help="CPU baseline: wall seconds per point of the core-count sweep")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-baseline-only", action="store_true",
+                   help="internal: run the CPU baseline sweep alone (no torch, no GPU) and print it")
     p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (rank 0, N=1 only)")
     p.add_argument("--e2e-segments", type=int, default=6)
     p.add_argument("--fused", action="store_true",
@@ -131,17 +133,20 @@ def _cpu_encode_until(args):
             return n, nbytes, time.time()
 
 
-def cpu_baseline(seconds: float):
+def cpu_baseline_sweep(seconds: float):
     """The oracle (kind "port": the C restatement of FFmpeg's mjpeg + swscale path, scalar
     C, one frame per process) on this host's cores, swept over process counts
     K in {1, usable/4, usable/2, usable}; each point runs `seconds` of wall time.  The value
-    is the best point.  FFmpeg itself (the reference CPU path) is absent on this pool."""
+    is the best point.  FFmpeg itself (the reference CPU path) is absent on this pool.
+    Runs in a process that never touched the GPU (cpu_baseline starts it as a child); the
+    pool's workers are closed and joined, never terminated."""
     import multiprocessing as mp
     hc = host_cpu()
     ks = sorted({1, max(1, hc["usable"] // 4), max(1, hc["usable"] // 2), hc["usable"]})
     ctx = mp.get_context("fork")
     sweep = []
-    with ctx.Pool(hc["usable"], initializer=_cpu_init) as pool:
+    pool = ctx.Pool(hc["usable"], initializer=_cpu_init)
+    try:
         pool.map(time.sleep, [0.01] * hc["usable"])  # every worker initialised
         for k in ks:
             t0 = time.time()
@@ -151,6 +156,9 @@ def cpu_baseline(seconds: float):
             sweep.append({"processes": k, "frames": frames, "seconds": round(dt, 2),
                           "value": round(frames / dt, 2),
                           "mean_jpeg_bytes": round(sum(b for _, b, _ in res) / max(frames, 1), 1)})
+    finally:
+        pool.close()  # workers exit on their own: no SIGTERM into forked children
+        pool.join()
     best = max(sweep, key=lambda s: s["value"])
     return {"value": best["value"], "unit": "frames/s", "cores": best["processes"], "kind": "port",
             "sample": f"{W}x{H}{'->%dx%d' % (DW, DH) if (DW, DH) != (W, H) else ''} "
@@ -160,6 +168,21 @@ def cpu_baseline(seconds: float):
                       f"path, not FFmpeg's SIMD encoder: FFmpeg is absent on this pool), one frame "
                       f"per process at a time",
             "host": hc, "sweep": sweep}
+
+
+def cpu_baseline(seconds: float, workload: str, huffman: str):
+    """cpu_baseline_sweep in a fresh interpreter (`bench.py --cpu-baseline-only`), which never
+    imports torch or HIP: the benchmark process has initialised the GPU, and forking pool
+    workers off it (round 3) left them with the GPU runtime's state and, under rocprofv3, the
+    profiler's signal handlers."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--workload", workload,
+           "--huffman", huffman, "--cpu-seconds", str(seconds)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=60 + 8 * seconds)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child exited {r.returncode}: {r.stderr[-1000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 # ------------------------------------------------------------------------ end to end
@@ -260,14 +283,22 @@ def frame_bytes(w, h):
     return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
 
 
-def load_pmc(workload, content):
+def load_pmc(workload, content, digest):
+    """profiles/pmc_<workload>.json's per-kernel counts, only when the file was counted on the
+    library this run loaded (its `library_digest` equals build.source_digest()); otherwise
+    ({}, reason) and every `traffic` is null: counters of another build are never reported."""
     if content != "testsrc":
-        return {}
+        return {}, "no PMC pass for this content"
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
-        with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json")) as f:
-            return json.load(f).get("kernels", {})
+        with open(path) as f:
+            d = json.load(f)
     except (OSError, ValueError):
-        return {}
+        return {}, f"no {os.path.relpath(path, ROOT)}"
+    if d.get("library_digest") != digest:
+        return {}, (f"{os.path.relpath(path, ROOT)} was counted on library {str(d.get('library_digest'))[:12]}, "
+                    f"this run loaded {digest[:12]}: traffic not reported")
+    return d.get("kernels", {}), os.path.relpath(path, ROOT)
 
 
 def pmc_traffic(pmc, *names):
@@ -332,6 +363,10 @@ def main():
         HUFF = "default"  # slice threading forces the default tables
     if a.seg is None:
         a.seg = SEG
+    if a.cpu_baseline_only:  # the child of cpu_baseline: nothing here touches the GPU
+        res = cpu_baseline_sweep(a.cpu_seconds)
+        print(json.dumps(res), flush=True)
+        return res
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -406,12 +441,13 @@ def main():
     frames_total = a.steps * seg * world
     value = frames_total / dt
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
-    pmc = load_pmc(a.workload, a.content) if (seg == SEG and not a.rst and not a.fused and a.dct == "auto"
-                                              and HUFF == WORKLOADS[a.workload][7]) else {}
+    pmc, pmc_src = (load_pmc(a.workload, a.content, B.source_digest())
+                    if (seg == SEG and not a.rst and not a.fused and a.dct == "auto"
+                        and HUFF == WORKLOADS[a.workload][7]) else ({}, "no PMC pass for this configuration"))
     overlap = HUFF == "optimal" or (DW, DH) != (W, H)  # two submit streams (see rooflines)
     primary, per_kernel = rooflines(kt, seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H),
                                     dt / a.steps * 1e3 if overlap else None)
-    primary = dict(primary, launches=nl)
+    primary = dict(primary, launches=nl, traffic_source=pmc_src)
 
     out = None
     if rank == 0:
@@ -424,7 +460,7 @@ def main():
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(a.cpu_seconds)
+                cpu = cpu_baseline(a.cpu_seconds, a.workload, HUFF)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"value": None, "error": repr(e)}
         content = {"testsrc": "testsrc2-like generator", "natural": "fractal (1/f) value noise",

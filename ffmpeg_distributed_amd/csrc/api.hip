@@ -187,7 +187,7 @@ struct Slot {
   uint64_t *d_frame_size = nullptr, *d_frame_offsets = nullptr;
   uint32_t *d_seg_size = nullptr;  // RST mode: stuffed segment sizes and offsets after the header
   uint32_t *d_seg_off = nullptr;
-  uint32_t *d_done = nullptr;      // k_count_ff's tickets: per segment, per frame, one per launch
+  uint32_t *d_done = nullptr;      // k_scan_ff's frame ticket (one word, zeroed by k_scan_bits)
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
   uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;  // optimal
@@ -418,7 +418,7 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
       (rc = dmalloc(&S.d_group_ff, B * NC)) || (rc = dmalloc(&S.d_ff_off, B * NC)) ||
       (rc = dmalloc(&S.d_frame_bits, B * NS)) || (rc = dmalloc(&S.d_status, 4)) ||
       (rc = dmalloc(&S.d_frame_size, B)) || (rc = dmalloc(&S.d_frame_offsets, B + 1)) ||
-      (rc = dmalloc(&S.d_done, B * NS + B + 1)) ||
+      (rc = dmalloc(&S.d_done, 1)) ||
       (rc = dmalloc(&S.d_work, (size_t)kXcds * kCtrStride)))
     return rc;
   HIP_TRY(hipMemset(S.d_work, 0, (size_t)kXcds * kCtrStride * sizeof(uint32_t)));
@@ -558,11 +558,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-#ifdef MJG_EXP_SERIAL_TAIL  // A/B: the tail on the submit stream (no co-run with the next k_encode)
-  c->tail = c->stream;
-#else
   HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));
-#endif
 
   c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
   const int cf = k.chroma_format;

@@ -418,7 +418,8 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
       row_pass<false>(raw, tab, nullptr, s_pk, lane);
       int dc = 0;
       uint32_t ca = 0, cb = 0;
-      if (active) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
+      uint32_t skip_st = 0xeu;  // every pair's skip test, every group
+      if (active) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb, skip_st, true);
       const uint64_t mask = screen_mask(ca, cb, s_scat);
       const int par = grp & 1;
       if (lane >= 56) s_dcx[par][wave][lane - 56] = dc;

@@ -1,16 +1,18 @@
 #pragma once
 // gfx950 kernels of the MJPEG segment encoder (see include/mjgpu.h for the boundary).
 //
-// Pipeline per submit (B frames, one launch per stage, all on the ctx stream):
+// Pipeline per submit (B frames; see DESIGN.md §4 for the streams they run on):
 //   k_scale       [only with -vf scale] bicubic hscale -> tv->pc range -> vscale, LDS-staged
-//   k_encode      one workgroup = one chunk of 64 MCUs (384 blocks, one 8x8 block per
-//                 thread): coalesced 8-byte row loads with edge replication, [tv->pc range],
-//                 integer jfdctint, quantiser, zigzag, DC prediction through LDS,
-//                 Huffman bit-length pass -> wave prefix-sum -> bit-pack pass into an
-//                 LDS window (ds_or_b32) -> chunk bitstream to a scratch slot
-//   k_scan_bits   per frame: exclusive scan of chunk bit lengths
-//   k_count_ff    per group of 32 chunks: realign the bits to the segment offset, pad with 1s,
-//                 count 0xFF; the last group of a segment / frame / launch sizes and places them
+//   k_encode      persistent waves, one chunk of 64 consecutive blocks (MCU coding order) per
+//                 wave step, lane = block: 8-byte row loads with edge replication, [tv->pc
+//                 range], jfdctint row pass (exact fp32) + column screen, exact quantisation of
+//                 the screened candidates, DC prediction by lane shuffles, Huffman coding,
+//                 wave prefix-sum bit-pack of the chunk into its scratch slot
+//   k_scan_bits   per segment: exclusive scan of chunk bit lengths
+//   k_count_ff    per group of 32 chunks: realign the bits to the segment offset (1-bit padding),
+//                 count 0xFF bytes
+//   k_scan_ff     per frame: scans of the group counts, segment / frame sizes; the last frame to
+//                 finish places every frame
 //   k_write       per group: header / stuffed scan bytes / RSTn / EOI into the packed output
 //
 // Arithmetic follows FFmpeg (see oracle/mjpeg_oracle.c for the per-function citations):
@@ -26,11 +28,7 @@ namespace mjg {
 constexpr int kEncWavesPerEU = 3;  // k_encode occupancy target (waves per SIMD); measured best (v8)
 
 constexpr int kMaxBlockBits = 1664;  // >= DC 16 + 63 * (16 + 10) bits
-#ifdef MJG_SLOT_WORDS  // layout experiments only (unsafe below the worst case)
-constexpr int kSlotWords = MJG_SLOT_WORDS;
-#else
 constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 blocks
-#endif
 
 // fp32 exact-integer arithmetic (k_encode): adding kM = 1.5*2^23 rounds to an integer
 // (round-to-nearest-even) and keeps it in the low mantissa bits; kMc = kM + 16384 leaves
@@ -480,10 +478,7 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
   int best_cost = serial;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-#ifndef MJG_EXP_WIDE_COST
-#define MJG_EXP_WIDE_COST 4
-#endif
-    const int cost = MJG_EXP_WIDE_COST * __popcll(hv[k]) + (4 << k);
+    const int cost = 4 * __popcll(hv[k]) + (4 << k);
     if (hv[k] && cost < best_cost) {
       best_cost = cost;
       best = hv[k];
@@ -634,10 +629,7 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
 // counters: c2 -6%, c5 -5% against 16; 8 and 24 measured too), 8 for the MFMA stage (3 waves
 // per SIMD, fewer chunks per wave), each the faster on its BASELINE configs
 template <bool MF>
-#ifndef MJG_EXP_BATCH
-#define MJG_EXP_BATCH 12
-#endif
-constexpr int kBatchOf = MF ? 8 : MJG_EXP_BATCH;
+constexpr int kBatchOf = MF ? 8 : 12;
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
 // quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
@@ -823,9 +815,7 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
 #pragma unroll
     for (int c = 0; c < 8; c++)
       s_pk[(c * 4 + rp) * 64 + lane] = __builtin_amdgcn_perm(__float_as_uint(b[c]), __float_as_uint(a[c]), 0x05040100u);
-#ifndef MJG_EXP_NO_SB_ROW
     __builtin_amdgcn_sched_barrier(0);
-#endif
   }
 }
 
@@ -836,13 +826,16 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
   // order; emit_block quantises the candidates exactly from the integer row image
   // (exact_coef).  Rows 0 and 4 (sums only) are exact, which gives the DC exactly:
   // (((x + 8) >> 4) + 32) >> 6 == floor((sum + 520) / 1024).
+// Adaptive skip test: st bit jp (wave-uniform, carried from chunk to chunk) records whether pair
+// jp's test skipped a column on the wave's previous test of it.  A pair is tested when it did,
+// or on every fourth chunk (retest); a pair whose columns are rarely skippable (detailed
+// content) then costs its test a quarter of the time (the test is ~20 VALU per pair).
 __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, const uint32_t *s_skip,
-                                              const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb) {
+                                              const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb,
+                                              uint32_t &st, bool retest) {
 #pragma unroll
   for (int jp = 0; jp < 4; jp++) {
-#ifndef MJG_EXP_NO_SB_PAIR
     __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time
-#endif
     uint32_t w[8];  // w[4h + i]: column 2jp + h of rows 2i (low half), 2i + 1 (high half)
 #pragma unroll
     for (int i = 0; i < 8; i++) w[i] = s_pk[(jp * 8 + i) * 64 + lane];
@@ -854,11 +847,7 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
     // max/min and saturating subtracts; a column is skipped when every block of the
     // chunk passes (wave ballot), its 8 screen bits are then 0.
     bool skip0 = false, skip1 = false;
-#ifdef MJG_EXP_NO_SKIP
-    if (false) {
-#else
-    if (jp > 0) {
-#endif
+    if (jp > 0 && (((st >> jp) & 1u) || retest)) {
       u16x2 ma = as_u16x2(w[0]), na = ma, mb = as_u16x2(w[4]), nb = mb;
 #pragma unroll
       for (int i = 1; i < 4; i++) {
@@ -878,12 +867,11 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
           as_u32(__builtin_elementwise_sub_sat(as_u16x2(s_skip[3 * jp - 1]), mn));
       skip0 = __ballot((t & 0xffffu) != 0u) == 0;
       skip1 = __ballot((t >> 16) != 0u) == 0;
+      st = (skip0 || skip1) ? st | (1u << jp) : st & ~(1u << jp);
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-#ifndef MJG_EXP_NO_SB_COL
       __builtin_amdgcn_sched_barrier(0);  // one column at a time
-#endif
       const int col = 2 * jp + h;
       if (h ? skip1 : skip0) {  // wave-uniform: 8 zero screen bits
         if (col < 4)
@@ -1246,6 +1234,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   uint64_t raw[8];
   bool fast = fetch_rows(raw, fb, ((uintptr_t)fb & 7) == 0, block_pos(g, bbase + b, s_bd), active);
   int carry = carry_finish(carry_row(fb, g, bbase, chunk, lane, s_bd), chunk, lane, rc, g, s_desc);
+  uint32_t skip_st = 0xeu;  // column_screen's adaptive skip test: test every pair first
 
   while (true) {
     // the next unit is reserved at the top of this unit's last chunk (its rows are prefetched
@@ -1282,7 +1271,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
 
     uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
     if (cur_active) {
-      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb);
+      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb, skip_st, (t & 3) == 0);
       if (DBG && g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
@@ -1756,14 +1745,8 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
 //               segment's last group its RSTn / EOI
 // The tail runs beside the next submit's k_encode, whose VALU issue it shares, so its cost per
 // word is kept to a few dozen VALU instructions per 64-word round (group_values).
-#ifndef MJG_TAIL_G
-#define MJG_TAIL_G 32
-#endif
-#ifndef MJG_TAIL_R
-#define MJG_TAIL_R 4
-#endif
-constexpr int kChunksPerWave = MJG_TAIL_G;  // chunks per group (lanes 0..G hold their metadata)
-constexpr int kTailRounds = MJG_TAIL_R;     // 64-word rounds whose slot loads are issued together
+constexpr int kChunksPerWave = 32;  // chunks per group (lanes 0..G hold their metadata)
+constexpr int kTailRounds = 4;      // 64-word rounds whose slot loads are issued together
 static_assert(kChunksPerWave * kSlotWords < (1 << 17), "group word offsets are 17-bit fields");
 
 // A group: chunks c0 .. c0 + n - 1 of segment s, owning words [k0, k1) of the segment's
@@ -1856,20 +1839,6 @@ __device__ __forceinline__ void group_values(const GroupWords &g, uint32_t kb, u
     const uint32_t off = (inf[i] >> 17) & 31u, rem = ((inf[i] >> 22) & 31u) + 1u;
     bnd[i] = valid && r + 1 == nsw;  // chunk c's last owned word
     own_nx[i] = valid && (lane == 63 || r + 1 == g.k1 - g.k0);  // lane + 1 does not hold word k + 1
-#ifdef MJG_EXP_BRANCHFREE
-    // 32-bit byte offsets from the group's first slot; X / B load A's word when not needed
-    const uint8_t *s0 = (const uint8_t *)g.slot0;
-    const uint32_t oa = __umul24((uint32_t)c, kSlotWords * 4u) + (wi << 2);
-    const bool nX = bnd[i] && off && rem > 32u - off;
-    const bool has_next = (inf[i] >> 27) & 1u;
-    const bool nB = own_nx[i] && (!bnd[i] || (rem < 32u && has_next));
-    const uint32_t ob = bnd[i] ? __umul24((uint32_t)c + 1u, kSlotWords * 4u) : oa + 4u;
-    A[i] = *(const uint32_t *)(s0 + oa);
-    X[i] = *(const uint32_t *)(s0 + (nX ? oa + 4u : oa));
-    B[i] = *(const uint32_t *)(s0 + (nB ? ob : oa));
-    X[i] = nX ? X[i] : 0u;
-    B[i] = nB ? B[i] : 0u;
-#else
     // 32-bit offsets from the group's first slot (the wave-uniform base: saddr loads)
     const uint8_t *s0 = (const uint8_t *)g.slot0;  // byte offsets < 2^32: one 32-bit VGPR each
     const uint32_t oa = (__umul24((uint32_t)c, (uint32_t)kSlotWords) + wi) << 2;
@@ -1879,7 +1848,6 @@ __device__ __forceinline__ void group_values(const GroupWords &g, uint32_t kb, u
     B[i] = (own_nx[i] && (!bnd[i] || (rem < 32u && has_next)))
                ? *(const uint32_t *)(s0 + (bnd[i] ? __umul24((uint32_t)c + 1u, (uint32_t)kSlotWords * 4u) : oa + 4u))
                : 0u;
-#endif
   }
 #pragma unroll
   for (int i = 0; i < R; i++) {
@@ -1948,9 +1916,7 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
       const uint32_t k = kb + 64 * i + lane;
       if (k < g.k1) {
         cnt += ff_bytes(v[i]);
-#ifndef MJG_EXP_COUNT_NOSTREAM
         *(uint32_t *)(sw + 4u * k) = v[i];
-#endif
       }
     }
   }
@@ -2008,11 +1974,14 @@ __global__ __launch_bounds__(256) void k_scan_ff(const uint32_t *__restrict__ gr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(done, 1u);
+    // release: this frame's size is visible (agent scope) before its ticket; acquire: the
+    // last ticket sees every frame's size
+    if (lane == 0) t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) s_last = t;
   }
   __syncthreads();
   if (s_last != (uint32_t)nframes - 1 || wave != 0) return;
+  __threadfence();  // every lane of the placing wave acquires the frame sizes (agent scope)
   // the last frame: packed offsets of every frame
   uint64_t carry = 0;
   for (int i0 = 0; i0 < nframes; i0 += 64) {
@@ -2115,14 +2084,8 @@ __global__ __launch_bounds__(256) void k_write(
       const uint32_t incl = wave_incl_scan(ff, lane);
       uint8_t *p = ob + 4 * (size_t)k + carry + incl - ff;
       const bool last = valid && 4 * k + 4 > total_bytes;  // the segment's last word: nb < 4 bytes
-#ifdef MJG_EXP_WRITE_NOSTORE
-      if (w == 0x12345678u && k == 7u) *(u32_any *)p = 0u;  // keeps the loads alive
-      else
-#endif
       if (valid && ff == 0 && !last) {
-#ifndef MJG_EXP_WRITE_NOSTORE
         *(u32_any *)p = __builtin_bswap32(w);
-#endif
       } else if (valid) {  // 0xFF bytes (each then 0x00), or the segment's last (short) word
         const uint32_t nb = min(4u, total_bytes - 4 * k);
         uint64_t X = 0;

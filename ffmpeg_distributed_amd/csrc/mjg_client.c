@@ -15,8 +15,13 @@
 // If no resident encoder listens (first segment, or it exited after its idle timeout), the
 // client starts one, with no descriptor of the segment inherited, and then connects.  This process never touches the GPU, so starting the encoder with fork + exec is
 // safe.  The socket lives in the abstract namespace; its name carries the user id, the device,
-// the visible-device environment, and the inode and mtime of libmjgpu.so, so a rebuilt library
-// or another device mapping gets a new encoder.  The encoder accepts only peers with its uid.
+// the visible-device environment, the process-level MJG_* settings the encoder reads once
+// (MJG_LIBRARY, MJG_NUMA_BIND, MJG_SERVE_BATCH_BYTES), and the inode and mtime of the library
+// it loads (MJG_LIBRARY or libmjgpu.so beside this client), so a rebuilt library, another
+// library or another device mapping gets a new encoder.  The abstract namespace has no file
+// permissions, so both sides check the peer: the encoder serves only its uid, and this client
+// hands its descriptors only to an encoder of its own uid (SO_PEERCRED).  The encoder's log is
+// /tmp/mjg-<uid>/<socket name>.log in a 0700 directory of this user (no symlinks followed).
 //
 //   mjg_client --device N [--python PATH] [--idle SECONDS] [--] <remote_args...>
 //   mjg_client --device N --shutdown        (asks a running encoder to exit; 0 if none runs)
@@ -25,7 +30,10 @@
 // Wire format (little-endian), client -> encoder, one message with SCM_RIGHTS {0, 1, 2}:
 //   "MJG1" u32 total_bytes u32 kind (0 encode, 1 shutdown) u32 nargs u32 nenv, then nargs
 //   NUL-terminated arguments and nenv NUL-terminated "NAME=VALUE" strings (the MJG_* settings
-//   of this process's environment); encoder -> client: i32 exit code.
+//   of this process's environment); encoder -> client: the byte 'A' once the request is read
+//   (before any of the segment is), then the i32 exit code.  A connection that ends before the
+//   'A' (an encoder closing its socket at its idle timeout while this client queued) touched
+//   nothing of the segment: the client connects again, starting an encoder if none listens.
 #define _GNU_SOURCE
 #include <errno.h>
 #include <fcntl.h>
@@ -74,7 +82,11 @@ static int self_dir(char *out, size_t cap) {
 
 static int sock_name(const char *dev, const char *pkg, char *name, size_t cap) {
   char lib[4200];
-  snprintf(lib, sizeof lib, "%s/libmjgpu.so", pkg);
+  const char *ml = getenv("MJG_LIBRARY");  // _lib.py loads this one instead when set
+  if (ml && *ml)
+    snprintf(lib, sizeof lib, "%s", ml);
+  else
+    snprintf(lib, sizeof lib, "%s/libmjgpu.so", pkg);
   struct stat st;
   if (stat(lib, &st) != 0) return -1;
   uint64_t h = 1469598103934665603ull;
@@ -82,6 +94,10 @@ static int sock_name(const char *dev, const char *pkg, char *name, size_t cap) {
   h = fnv(h, getenv("ROCR_VISIBLE_DEVICES"));
   h = fnv(h, getenv("CUDA_VISIBLE_DEVICES"));
   h = fnv(h, getenv("GPU_DEVICE_ORDINAL"));
+  // settings the encoder process reads once at import (worker.py, _lib.py)
+  h = fnv(h, ml);
+  h = fnv(h, getenv("MJG_NUMA_BIND"));
+  h = fnv(h, getenv("MJG_SERVE_BATCH_BYTES"));
   snprintf(name, cap, "mjg-gpu-%u-%s-%llx-%llx-%llx", (unsigned)getuid(), dev, (unsigned long long)st.st_ino,
            (unsigned long long)st.st_mtim.tv_sec * 1000000000ull + (unsigned long long)st.st_mtim.tv_nsec,
            (unsigned long long)h);
@@ -101,7 +117,24 @@ static int try_connect(const char *name) {
     close(fd);
     return -e;
   }
+  // the abstract namespace has no permissions: hand descriptors only to our own uid
+  struct ucred cr;
+  socklen_t cl = sizeof cr;
+  if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &cl) != 0 || cr.uid != getuid()) {
+    close(fd);
+    return -EACCES;
+  }
   return fd;
+}
+
+// /tmp/mjg-<uid>: created 0700, and used only when it is a real directory of this user with no
+// access for others (not a symlink another user planted)
+static int log_dir(char *out, size_t cap) {
+  snprintf(out, cap, "/tmp/mjg-%u", (unsigned)getuid());
+  if (mkdir(out, 0700) != 0 && errno != EEXIST) return -1;
+  struct stat st;
+  if (lstat(out, &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != getuid() || (st.st_mode & 077)) return -1;
+  return 0;
 }
 
 // Start the resident encoder: cwd = the package's parent (python -m finds the package there),
@@ -109,17 +142,22 @@ static int try_connect(const char *name) {
 // EOF on this process's stderr), no other descriptor inherited.  It stays in the caller's
 // process group (no setsid): whoever stops the dispatcher's job by its group stops the encoder
 // too, and otherwise it ends after its idle timeout.
-static pid_t spawn(const char *python, const char *pkg, const char *dev, const char *name, const char *idle) {
-  char root[4096], logp[256];
+static pid_t spawn(const char *python, const char *pkg, const char *dev, const char *name, const char *idle,
+                   const char *logp) {
+  char root[4096];
   snprintf(root, sizeof root, "%s", pkg);
   char *s = strrchr(root, '/');
   if (!s) return -1;
   *s = 0;
-  snprintf(logp, sizeof logp, "/tmp/%s.log", name);
   const pid_t pid = fork();
   if (pid != 0) return pid;
   const int nul = open("/dev/null", O_RDONLY);
-  int log = open(logp, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0600);
+  int log = *logp ? open(logp, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC | O_NOFOLLOW, 0600) : -1;
+  struct stat st;
+  if (log >= 0 && (fstat(log, &st) != 0 || !S_ISREG(st.st_mode) || st.st_uid != getuid())) {
+    close(log);
+    log = -1;
+  }
   if (log < 0) log = open("/dev/null", O_WRONLY);
   if (nul < 0 || chdir(root) != 0) _exit(126);
   dup2(nul, 0);
@@ -202,27 +240,8 @@ int main(int argc, char **argv) {
     return 0;
   }
 
-  int sk = try_connect(name);
-  if (sk < 0 && shutdown_req) return 0;  // nothing runs
-  pid_t child = -1;
-  if (sk < 0) {
-    child = spawn(python, pkg, dev, name, idle);
-    if (child < 0) return die(dev, "cannot start the resident encoder", errno);
-    const struct timespec ts = {0, 2000000};  // 2 ms
-    for (int i = 0; i < 60000 && sk < 0; i++) {  // up to ~2 min (first start: imports + HIP init)
-      nanosleep(&ts, NULL);
-      sk = try_connect(name);
-      int st;
-      if (sk < 0 && child > 0 && waitpid(child, &st, WNOHANG) == child) {
-        child = -1;  // exited: lost the bind race to another encoder (exit 0), or failed
-        if (!(WIFEXITED(st) && WEXITSTATUS(st) == 0)) {
-          fprintf(stderr, "gpu:%s: resident encoder failed to start (log: /tmp/%s.log)\n", dev, name);
-          return 1;
-        }
-      }
-    }
-    if (sk < 0) return die(dev, "resident encoder did not come up", -sk);
-  }
+  char logp[4400] = "", ldir[64];
+  if (log_dir(ldir, sizeof ldir) == 0) snprintf(logp, sizeof logp, "%s/%s.log", ldir, name);
 
   // request: header, arguments, MJG_* environment
   size_t len = 20, nargs = (size_t)(argc - a), nenv = 0;
@@ -251,9 +270,47 @@ int main(int argc, char **argv) {
       memcpy(p, *e, n);
       p += n;
     }
-  const int rc_send = send_all_fds(sk, buf, len, !shutdown_req);
+
+  int sk = -1;
+  pid_t child = -1;
+  for (int attempt = 0;; attempt++) {
+    sk = try_connect(name);
+    if (sk == -EACCES) return die(dev, "the encoder socket belongs to another user; not sending the segment", 0);
+    if (sk < 0 && shutdown_req) return 0;  // nothing runs
+    if (sk < 0) {
+      child = spawn(python, pkg, dev, name, idle, logp);
+      if (child < 0) return die(dev, "cannot start the resident encoder", errno);
+      const struct timespec ts = {0, 2000000};  // 2 ms
+      for (int i = 0; i < 60000 && sk < 0; i++) {  // up to ~2 min (first start: imports + HIP init)
+        nanosleep(&ts, NULL);
+        sk = try_connect(name);
+        if (sk == -EACCES) return die(dev, "the encoder socket belongs to another user; not sending the segment", 0);
+        int st;
+        if (sk < 0 && child > 0 && waitpid(child, &st, WNOHANG) == child) {
+          child = -1;  // exited: lost the bind race to another encoder (exit 0), or failed
+          if (!(WIFEXITED(st) && WEXITSTATUS(st) == 0)) {
+            fprintf(stderr, "gpu:%s: resident encoder failed to start (log: %s)\n", dev, *logp ? logp : "none");
+            return 1;
+          }
+        }
+      }
+      if (sk < 0) return die(dev, "resident encoder did not come up", -sk);
+    }
+    const int rc_send = send_all_fds(sk, buf, len, !shutdown_req);
+    unsigned char ack = 0;
+    ssize_t k = -1;
+    if (rc_send == 0)
+      do k = read(sk, &ack, 1);
+      while (k < 0 && errno == EINTR);
+    if (k == 1 && ack == 'A') break;
+    close(sk);
+    // no 'A': the encoder closed this connection unread (idle exit); nothing of the segment
+    // was consumed, so connect again (a few times at most)
+    if (attempt == 3) return die(dev, "the resident encoder keeps closing the connection", rc_send < 0 ? -rc_send : 0);
+    const struct timespec ts = {0, 20000000};  // 20 ms
+    nanosleep(&ts, NULL);
+  }
   free(buf);
-  if (rc_send < 0) return die(dev, "cannot send the segment to the resident encoder", -rc_send);
 
   unsigned char r[4];
   size_t got = 0;

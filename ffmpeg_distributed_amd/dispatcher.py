@@ -1,7 +1,11 @@
 """Segment dispatcher: the reference's split -> per-host worker queue -> concat flow
 (Rouji/ffmpeg_distributed, ffmpeg_distributed.py:150-236) with one addition: a host
-named `gpu:N` runs the MI355X worker (`python -m ffmpeg_distributed_amd.worker
---device N <remote_args>`) as a local process instead of `ssh HOST ffmpeg ...`.
+named `gpu:N` runs a local per-segment process instead of `ssh HOST ffmpeg ...`:
+`mjg_client --device N --python PY -- <remote_args>` (csrc/mjg_client.c), which hands its
+stdin / stdout / stderr to GPU N's resident encoder (resident.py), or, when the client is
+not built or MJG_RESIDENT=0, `python -m ffmpeg_distributed_amd.worker --device N
+<remote_args>` (worker_argv; INTEGRATION.md §1 is the same argv as a patch to the
+reference, pinned by the gpu_* fixtures).
 
 Everything observable is kept as in the reference and pinned by
 tests/golden/reference_dispatch.json (captured from the reference itself):

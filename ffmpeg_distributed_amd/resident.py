@@ -15,8 +15,11 @@ NAME, an abstract-namespace socket.  Each connection is one request (wire format
 mjg_client.c): an encode request carries the remote_args, the client's MJG_* environment
 and its three descriptors; `worker.run` encodes the segment from them on a thread of its
 own (segments of concurrent clients overlap on the GPU), the copies of the descriptors are
-closed, then the exit code goes back.  Peers with another uid are refused.  The encoder
-exits after `idle` seconds without a request, or on a shutdown request.
+closed, then the exit code goes back (an 'A' byte acknowledges the request first: a client
+whose connection closes before it, queued while the encoder shut its socket at the idle
+timeout, connects again).  Peers with another uid are refused (and the client refuses an
+encoder of another uid).  The encoder exits after `idle` seconds without a request, or on a
+shutdown request.
 """
 from __future__ import annotations
 
@@ -38,6 +41,7 @@ MAGIC = b"MJG1"
 KIND_ENCODE, KIND_SHUTDOWN = 0, 1
 HEADER = struct.Struct("<4sIIII")   # magic, total bytes, kind, nargs, nenv
 MAX_REQUEST = 1 << 20
+ACK = b"A"                           # request read: the client no longer retries the connection
 MAX_IDLE_CACHES = 4                  # encoder contexts kept between segments
 
 
@@ -138,6 +142,7 @@ class Resident:
                 return
             data, fds = recv_request(conn)
             kind, args, env = parse_request(data)
+            conn.sendall(ACK)  # read, nothing of the segment touched yet (see mjg_client.c)
             if kind == KIND_SHUTDOWN:
                 self.stop.set()
                 rc = 0

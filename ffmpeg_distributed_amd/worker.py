@@ -247,7 +247,7 @@ def _pread_exact(fd: int, dest, off: int) -> None:
 class Source:
     """Packed planar frames from stdin: .info (StreamInfo), .read_into(buf, n) -> count."""
 
-    def __init__(self, raw, read_threads: int = READ_THREADS):
+    def __init__(self, raw, read_threads: int = READ_THREADS, stderr=None):
         self.child = None
         self.feeder = None
         head = raw.read(4)
@@ -275,7 +275,8 @@ class Source:
                 self.read_into = self._read_mkv_pread
             return
         # any other codec: ffmpeg decodes, we read its y4m
-        self.child = subprocess.Popen(DECODE_ARGV, stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+        self.child = subprocess.Popen(DECODE_ARGV, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                      stderr=_fd_or_none(stderr))
         self.feeder = threading.Thread(target=self._feed, args=(mkv, raw), daemon=True)
         self.feeder.start()
         self._y4m(container.Y4MReader(self.child.stdout))
@@ -361,24 +362,34 @@ def _fd_or_none(f):
         return None
 
 
-def passthrough(args: List[str], stdin=None, stdout=None) -> int:
+def passthrough(args: List[str], stdin=None, stdout=None, stderr=None) -> int:
     """Outside the GPU profile: run exactly what the reference runs (on this segment's
-    input and output files: the process's own stdin/stdout unless given)."""
+    input, output and error streams: the process's own stdin / stdout / stderr unless given;
+    in the resident encoder they are the client's descriptors, so ffmpeg's own `Duration:` /
+    `frame=` lines reach the dispatcher as they would from the reference's worker)."""
+    err = stderr or sys.stderr
+    err.flush()  # our own lines before the child's
     try:
-        return subprocess.call(reference_argv(args), stdin=_fd_or_none(stdin), stdout=_fd_or_none(stdout))
+        return subprocess.call(reference_argv(args), stdin=_fd_or_none(stdin), stdout=_fd_or_none(stdout),
+                               stderr=_fd_or_none(err))
     except FileNotFoundError:
-        sys.stderr.write("ffmpeg not found for a non-GPU profile\n")
+        err.write("ffmpeg not found for a non-GPU profile\n")
+        err.flush()
         return 127
 
 
-def ffmpeg_fallthrough(src: Source, args: List[str], stdout) -> int:
+def ffmpeg_fallthrough(src: Source, args: List[str], stdout, stderr=None) -> int:
     """The reference command on the CPU for frames already being read: the decoded frames
-    go to `ffmpeg -f yuv4mpegpipe -i pipe: <remote_args> -f matroska pipe:` as y4m."""
+    go to `ffmpeg -f yuv4mpegpipe -i pipe: <remote_args> -f matroska pipe:` as y4m (its
+    stderr is the segment's, see passthrough)."""
+    err = stderr or sys.stderr
     argv = ["ffmpeg", "-f", "yuv4mpegpipe", "-i", "pipe:", *args, "-f", "matroska", "pipe:"]
+    err.flush()
     try:
-        child = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=stdout)
+        child = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=stdout, stderr=_fd_or_none(err))
     except FileNotFoundError:
-        sys.stderr.write("ffmpeg not found for a non-GPU profile\n")
+        err.write("ffmpeg not found for a non-GPU profile\n")
+        err.flush()
         src.close()
         return 127
     fb = src.info.frame_bytes
@@ -413,15 +424,15 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     if prof is None:
         stderr.write(f"gpu:{device}: {why}; running ffmpeg on the CPU\n")
         stderr.flush()
-        return passthrough(args, stdin, stdout)
+        return passthrough(args, stdin, stdout, stderr)
 
-    src = Source(stdin, opts.read_threads)
+    src = Source(stdin, opts.read_threads, stderr)
     info = src.info
     if prof.chroma is not None and prof.chroma != info.chroma:
         stderr.write(f"gpu:{device}: -pix_fmt needs {info.chroma} -> {prof.chroma} chroma resampling; "
                      f"running ffmpeg on the CPU\n")
         stderr.flush()
-        return ffmpeg_fallthrough(src, args, stdout)
+        return ffmpeg_fallthrough(src, args, stdout, stderr)
     dst_w, dst_h = prof.scale or (info.width, info.height)
     bind_numa(device)  # before the reader threads and the batch buffers
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here

@@ -5,6 +5,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -85,3 +86,26 @@ def test_open_without_gpu_fails_loudly():
     from ffmpeg_distributed_amd.encoder import MjpegEncoder
     with pytest.raises(_lib.MjgError):
         MjpegEncoder(0, 64, 48)
+
+
+def test_product_kernels_carry_no_experiment_switches():
+    """The shipped kernel sources hold no preprocessor branches (experiments live as source
+    patches in tools/patches.py, applied to a copy for tools/variants.py A/Bs)."""
+    import glob
+    import re
+    csrc = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
+    bad = []
+    for p in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))
+                    + glob.glob(os.path.join(csrc, "*.cpp"))):
+        for i, line in enumerate(open(p), 1):
+            if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b", line):
+                bad.append(f"{os.path.basename(p)}:{i}: {line.strip()}")
+    assert not bad, bad
+
+
+def test_experiment_patches_still_apply():
+    """Every tools/patches.py experiment anchors exactly once in the product source."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import patches
+    res = patches.check_all()
+    assert all(res.values()), [k for k, v in res.items() if not v]

@@ -81,7 +81,10 @@ def canon_calls(calls):
     return seq, workers, ssh
 
 
-@pytest.mark.parametrize("name", sorted(FX["scenarios"]))
+PATCHED = sorted(n for n, v in FX["scenario_patched"].items() if v)
+
+
+@pytest.mark.parametrize("name", sorted(set(FX["scenarios"]) - set(PATCHED)))
 def test_dispatcher_matches_reference(name):
     ref = json.loads(norm_md5(json.dumps(FX["scenarios"][name])))
     ours, err = run_ours(name)
@@ -126,3 +129,37 @@ def test_cli_quirk_copy_flag_needs_double_dash():
         D.build_parser().parse_args(["-H", "localhost", "in", "out", "-c:v mjpeg", "-an"])
     a = D.build_parser().parse_args(["-H", "gpu:0", "-H", "gpu:1", "--", "in", "out", "-c:v mjpeg", "-an"])
     assert a.host == ["gpu:0", "gpu:1"] and a.remote_args == "-c:v mjpeg" and a.segment_length == 10
+
+
+def _integration_patch():
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    i = text.index("# ffmpeg_distributed.py, TaskThread.run, replacing lines 131-138")
+    return [l for l in text[i:text.index("```", i)].splitlines()[1:] if l.strip()]
+
+
+def test_integration_patch_is_the_one_pinned():
+    """INTEGRATION.md §1's patch is the text the gpu_* fixtures ran inside the reference."""
+    assert FX["integration_patch"] == _integration_patch()
+
+
+@pytest.mark.parametrize("name", PATCHED)
+def test_patched_reference_gpu_argv_is_worker_argv(name):
+    """The reference patched as INTEGRATION.md says builds, for -H gpu:N, exactly the argv
+    dispatcher.worker_argv builds (mjg_client -> the GPU's resident encoder; with
+    MJG_RESIDENT=0 one Python worker per segment), and the rest of its flow is unchanged."""
+    sc = FX["scenarios"][name]
+    resident = FX["scenario_env"][name].get("MJG_RESIDENT", "1") != "0"
+    args = __import__("shlex").split(FX["remote_args"])
+    workers = [c for c in sc["calls"] if c["prog"] != "ffmpeg"]
+    hosts = [FX["scenario_args"][name][i + 1] for i, a in enumerate(FX["scenario_args"][name]) if a == "-H"]
+    expect = {}
+    for h in hosts:
+        argv = D.worker_argv(h, args, resident=resident)
+        expect[h] = [a.replace(os.path.dirname(D.CLIENT), "<PKG>") if a == D.CLIENT else
+                     "<PYTHON>" if a == sys.executable else a for a in argv]
+    assert workers and all(c["argv"] in expect.values() for c in workers), (workers, expect)
+    assert len(workers) == sc["output"].count("GPU[")  # one worker per segment, none retried
+    assert sc["returncode"] == 0 and not sc["stderr_has_failure_report"]
+    # split and concat calls are the unpatched reference's
+    base = FX["scenarios"]["basic_two_hosts"]["calls"]
+    assert [c for c in sc["calls"] if c["prog"] == "ffmpeg"][0] == base[0]

@@ -179,3 +179,66 @@ def test_worker_argv_resident_switch(client, monkeypatch):
     monkeypatch.setenv("MJG_RESIDENT", "1")
     assert D.worker_argv("gpu:2", args) == [client, "--device", "2", "--python", sys.executable, "--", *args]
     assert D.server_argv("gpu:2", args)[-1] == "--serve"
+
+
+def test_resident_passthrough_progress_reaches_the_client(client, tmp_path, monkeypatch):
+    """A non-GPU profile in the resident encoder runs the real worker.run, which runs the
+    reference's ffmpeg command (here the tests/shims stand-in) on the segment's descriptors:
+    ffmpeg's own Duration / frame= lines and its output reach the client's stderr / stdout,
+    not the encoder's log (worker.passthrough inherited the resident's stderr)."""
+    monkeypatch.setenv("PATH", os.path.join(ROOT, "tests", "shims") + os.pathsep + os.environ["PATH"])
+    name = socket_name(client)
+    srv = R.Resident(0, R.listen(name), idle=60)  # run = worker.run
+    th = threading.Thread(target=srv.serve, daemon=True)
+    th.start()
+    try:
+        argv = D.worker_argv("gpu:0", ["-c:v", "libx264", "-crf", "18"], resident=True)
+        (tmp_path / "in").write_bytes(b"SEGMENT")
+        rc, p, seen = run_segment(argv, tmp_path / "in", tmp_path / "out")
+        assert rc == 0, p.stderr
+        assert (tmp_path / "out").read_bytes() == b"ENC[SEGMENT]"
+        assert p.duration == 10.0 and [s[0] for s in seen] == [50, 100]
+        assert "gpu:0: " in p.stderr and "running ffmpeg on the CPU" in p.stderr
+        monkeypatch.setenv("PATH", "/nonexistent")  # no ffmpeg: the message is the segment's too
+        rc, p, _ = run_segment(argv, tmp_path / "in", tmp_path / "out2")
+        assert rc == 127 and "ffmpeg not found" in p.stderr
+    finally:
+        subprocess.run([client, "--device", "0", "--shutdown"])
+        th.join(10)
+
+
+def test_client_reconnects_when_a_connection_closes_before_the_ack(client, tmp_path):
+    """An encoder that closes a queued connection unread (its idle exit racing a client) ends
+    that connection before the 'A' acknowledgement: nothing of the segment was read, so the
+    client connects again and the segment is encoded once, with exit code 0."""
+    name = socket_name(client)
+    sock = R.listen(name)
+    dropped = []
+
+    def serve():
+        conn, _ = sock.accept()  # the first connection: closed unread
+        dropped.append(1)
+        conn.close()
+        R.Resident(0, sock, idle=60, run=fake_run).serve()
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    try:
+        argv = D.worker_argv("gpu:0", ["-q:v", "5"], resident=True)
+        (tmp_path / "in").write_bytes(b"seg")
+        rc, p, _ = run_segment(argv, tmp_path / "in", tmp_path / "out")
+        assert rc == 0 and dropped == [1], p.stderr
+        assert (tmp_path / "out").read_bytes() == b"GPU0:seg:1"
+    finally:
+        subprocess.run([client, "--device", "0", "--shutdown"])
+        th.join(10)
+
+
+def test_client_log_is_private(client):
+    """The encoder's log lives in a 0700 directory of this user (no symlink followed)."""
+    import stat
+    d = f"/tmp/mjg-{os.getuid()}"
+    subprocess.run([client, "--device", "0", "--socket-name"], check=True, capture_output=True)
+    if os.path.exists(d):
+        st = os.lstat(d)
+        assert stat.S_ISDIR(st.st_mode) and st.st_uid == os.getuid() and (st.st_mode & 0o077) == 0

@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Source patches of the encoder's measured-and-not-kept experiments, applied to a copy of
+ffmpeg_distributed_amd/csrc for tools/variants.py A/Bs.  The product kernels carry no
+experiment switches (no `#if` but include guards); each former MJG_EXP_* / MJG_TAIL_* /
+MJG_SLOT_WORDS branch lives here as exact text replacements, so an old A/B can be re-run
+with `VARIANTS="base=:;x=@no_skip"` (several: `@no_sb_row+no_sb_col`, parameters:
+`@wide_cost=3`).
+
+A patch is a list of (file, old, new); `old` must occur exactly once (the patch fails loudly
+when the product source has moved on)."""
+from __future__ import annotations
+
+import os
+import shutil
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
+K = "kernels.hip"
+
+
+# name -> function(param or None) -> [(file, old, new)]
+PATCHES = {
+    # the stuffing tail on the submit stream: no co-run with the next submit's k_encode
+    # (profiles/r03_ab_serial_tail.txt)
+    "serial_tail": lambda a: [("api.hip", "  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));\n",
+                               "  c->tail = c->stream;\n")],
+    # no column skip test in the VALU column screen (profiles/r03_ab_column_skip.txt)
+    "no_skip": lambda a: [(K, "    if (jp > 0 && (((st >> jp) & 1u) || retest)) {\n", "    if (false) {\n")],
+    # the column skip test on every chunk (round 3's form, before the adaptive test)
+    "always_test": lambda a: [(K, "    if (jp > 0 && (((st >> jp) & 1u) || retest)) {\n", "    if (jp > 0) {\n")],
+    # wave-parallel block cost factor (profiles/r03_ab_wide_cost.txt)
+    "wide_cost": lambda a: [(K, "const int cost = 4 * __popcll(hv[k])", f"const int cost = {int(a)} * __popcll(hv[k])")],
+    # chunks per k_encode work unit, VALU stage (profiles/r03_ab_sched_units.txt)
+    "batch": lambda a: [(K, "constexpr int kBatchOf = MF ? 8 : 12;", f"constexpr int kBatchOf = MF ? 8 : {int(a)};")],
+    # k_encode scheduling barriers (profiles/r03_ab_sched_units.txt)
+    "no_sb_row": lambda a: [(K, "0x05040100u);\n    __builtin_amdgcn_sched_barrier(0);\n", "0x05040100u);\n")],
+    "no_sb_pair": lambda a: [(K, "    __builtin_amdgcn_sched_barrier(0);  // one column pair in flight at a time\n", "")],
+    "no_sb_col": lambda a: [(K, "      __builtin_amdgcn_sched_barrier(0);  // one column at a time\n", "")],
+    # stuffing tail group size / rounds
+    "tail_g": lambda a: [(K, "constexpr int kChunksPerWave = 32;", f"constexpr int kChunksPerWave = {int(a)};")],
+    "tail_r": lambda a: [(K, "constexpr int kTailRounds = 4;", f"constexpr int kTailRounds = {int(a)};")],
+    # slot stride (words per chunk).  UNSAFE below the worst case 3328: layout timing only
+    "slot_words": lambda a: [(K, "constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;",
+                              f"constexpr int kSlotWords = {int(a)};")],
+    # k_count_ff without its realigned-stream stores (timing probe: k_write then reads garbage)
+    "count_nostream": lambda a: [(K, "        cnt += ff_bytes(v[i]);\n        *(uint32_t *)(sw + 4u * k) = v[i];\n",
+                                  "        cnt += ff_bytes(v[i]);\n")],
+    # k_write without its clean-word stores (timing probe: wrong output)
+    "write_nostore": lambda a: [(K, "      if (valid && ff == 0 && !last) {\n        *(u32_any *)p = __builtin_bswap32(w);\n      }",
+                                 "      if (w == 0x12345678u && k == 7u) *(u32_any *)p = 0u;  // keeps the loads alive\n"
+                                 "      else if (valid && ff == 0 && !last) {\n      }")],
+    # branch-free slot loads in k_count_ff (measured slower)
+    "branchfree": lambda a: [(K, """    // 32-bit offsets from the group's first slot (the wave-uniform base: saddr loads)
+    const uint8_t *s0 = (const uint8_t *)g.slot0;  // byte offsets < 2^32: one 32-bit VGPR each
+    const uint32_t oa = (__umul24((uint32_t)c, (uint32_t)kSlotWords) + wi) << 2;
+    A[i] = *(const uint32_t *)(s0 + oa);
+    X[i] = (bnd[i] && off && rem > 32u - off) ? *(const uint32_t *)(s0 + oa + 4u) : 0u;
+    const bool has_next = (inf[i] >> 27) & 1u;
+    B[i] = (own_nx[i] && (!bnd[i] || (rem < 32u && has_next)))
+               ? *(const uint32_t *)(s0 + (bnd[i] ? __umul24((uint32_t)c + 1u, (uint32_t)kSlotWords * 4u) : oa + 4u))
+               : 0u;
+""", """    // 32-bit byte offsets from the group's first slot; X / B load A's word when not needed
+    const uint8_t *s0 = (const uint8_t *)g.slot0;
+    const uint32_t oa = __umul24((uint32_t)c, kSlotWords * 4u) + (wi << 2);
+    const bool nX = bnd[i] && off && rem > 32u - off;
+    const bool has_next = (inf[i] >> 27) & 1u;
+    const bool nB = own_nx[i] && (!bnd[i] || (rem < 32u && has_next));
+    const uint32_t ob = bnd[i] ? __umul24((uint32_t)c + 1u, kSlotWords * 4u) : oa + 4u;
+    A[i] = *(const uint32_t *)(s0 + oa);
+    X[i] = *(const uint32_t *)(s0 + (nX ? oa + 4u : oa));
+    B[i] = *(const uint32_t *)(s0 + (nB ? ob : oa));
+    X[i] = nX ? X[i] : 0u;
+    B[i] = nB ? B[i] : 0u;
+""")],
+    # occupancy probe: k_encode's workgroup LDS past 40 KB (3 workgroups, 3 waves per SIMD)
+    "occ3": lambda a: [(K, "  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];",
+                        "  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords + 512];")],
+}
+
+# ---------------------------------------------------------------- probes (wrong timing, right bytes)
+# phase_clock: k_encode<.., kEmitDefault> lane 0 reads the shader clock (s_memtime) at the phase
+# boundaries of every chunk and adds the deltas into mjg_phase_acc[8] (one atomic per phase per
+# wave at its end); mjg_probe_phase() returns and clears them (tools/phase_probe.py).  The clock
+# reads wait for the wave's outstanding LDS / scalar operations (lgkmcnt), so each phase also
+# absorbs the LDS latency still open at its end.
+_PH_DECL = "constexpr int kWavesPerWg = 4;\n"
+_PH_DEVICE = (_PH_DECL + "__device__ unsigned long long mjg_phase_acc[8];\n"
+              "#define MJG_PH(i) do { if (MODE == kEmitDefault) { __builtin_amdgcn_sched_barrier(0); "
+              "const unsigned long long _t = __builtin_amdgcn_s_memtime(); ph_acc[i] += _t - ph_prev; ph_prev = _t; "
+              "__builtin_amdgcn_sched_barrier(0); } } while (0)\n")
+
+
+def _phase_clock(a):
+    return [
+        (K, _PH_DECL, _PH_DEVICE),
+        (K, "  while (true) {\n    // the next unit is reserved",
+         "  unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_prev = __builtin_amdgcn_s_memtime();\n"
+         "  while (true) {\n    MJG_PH(7);\n    // the next unit is reserved"),
+        (K, "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);\n", "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);\n    MJG_PH(0);\n"),
+        (K, "    uint32_t ca = 0, cb = 0;  // screen bits", "    MJG_PH(1);\n    uint32_t ca = 0, cb = 0;  // screen bits"),
+        (K, "    if (SCR) mask = screen_mask(ca, cb, s_scat);\n", "    if (SCR) mask = screen_mask(ca, cb, s_scat);\n    MJG_PH(2);\n"),
+        (K, "    if (cur_active && !((wide >> lane) & 1ull)) {", "    MJG_PH(3);\n    if (cur_active && !((wide >> lane) & 1ull)) {"),
+        (K, "    if (wide) {  // the heavy blocks", "    MJG_PH(4);\n    if (wide) {  // the heavy blocks"),
+        (K, "    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    if (tn < 0) break;",
+         "    MJG_PH(5);\n    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    MJG_PH(6);\n"
+         "    if (tn < 0) break;"),
+        (K, "  if (MODE == kCount && aux_frame >= 0) {\n    asm volatile",
+         "  if (MODE == kEmitDefault && lane == 0)\n    for (int i = 0; i < 8; i++) atomicAdd(&mjg_phase_acc[i], ph_acc[i]);\n"
+         "  if (MODE == kCount && aux_frame >= 0) {\n    asm volatile"),
+        ("api.hip", "}  // extern \"C\"", "int mjg_probe_phase(unsigned long long *out) {\n"
+         "  HIP_TRY(hipDeviceSynchronize());\n  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(mjg_phase_acc), 64));\n"
+         "  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mjg_phase_acc), z, 64));\n"
+         "  return MJG_OK;\n}\n}  // extern \"C\""),
+    ]
+
+
+PATCHES["phase_clock"] = _phase_clock
+
+
+def parse_spec(spec: str):
+    """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
+    out = []
+    for item in spec.split("+"):
+        name, _, arg = item.partition("=")
+        if name not in PATCHES:
+            raise KeyError(f"unknown patch {name!r} (known: {', '.join(sorted(PATCHES))})")
+        out.append((name, arg or None))
+    return out
+
+
+def apply(spec: str, dst: str, src: str = CSRC) -> str:
+    """Copy `src` (the product csrc) to `dst` and apply the patches of `spec`; returns dst."""
+    if os.path.isdir(dst):
+        shutil.rmtree(dst)
+    shutil.copytree(src, dst)
+    for name, arg in parse_spec(spec):
+        for fname, old, new in PATCHES[name](arg):
+            path = os.path.join(dst, fname)
+            with open(path) as f:
+                text = f.read()
+            n = text.count(old)
+            if n != 1:
+                raise ValueError(f"patch {name}: anchor found {n} times in {fname}")
+            with open(path, "w") as f:
+                f.write(text.replace(old, new))
+    return dst
+
+
+def check_all() -> dict:
+    """Every patch's anchors against the current product source (tests/test_abi.py)."""
+    res = {}
+    for name, fn in PATCHES.items():
+        edits = fn("1")
+        ok = True
+        for fname, old, _ in edits:
+            with open(os.path.join(CSRC, fname)) as f:
+                ok &= f.read().count(old) == 1
+        res[name] = ok
+    return res
+
+
+if __name__ == "__main__":
+    import json
+    print(json.dumps(check_all(), indent=1))

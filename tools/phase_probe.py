@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-phase wall cycles of k_encode (VALU stage, -huffman default) from the phase_clock probe
+patch (tools/patches.py): VARIANTS="ph=@phase_clock" tools/variants.py --build, then this on the
+GPU box.  For each WL/CONTENT: 3 synced submits, shader-clock cycles per chunk-wave per phase
+(wall time of the wave, so other waves' issue on the SIMD is included).
+
+usage: WL=c2 CONTENT=testsrc python3 tools/phase_probe.py [variant-name ...]   (default: ph)"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PHASES = ["row pass (+ edge refetch)", "next chunk's loads issued", "column screen + mask",
+          "DC prediction + wide-block choice", "per-lane emission", "wave-parallel blocks",
+          "pack", "unit bookkeeping + loop"]
+
+
+def main():
+    import torch
+    import bench
+    from ffmpeg_distributed_amd import _lib
+    from ffmpeg_distributed_amd.testsrc import CONTENT
+    names = sys.argv[1:] or ["ph"]
+    W, H, DW, DH, Q, N, FULL, HUFF, _ = bench.WORKLOADS[os.environ.get("WL", "c2")]
+    content = os.environ.get("CONTENT", "testsrc")
+    dev = torch.device("cuda", 0)
+    pool = torch.empty((N, W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2)), dtype=torch.uint8, device=dev)
+    for i in range(0, N, 10):
+        k = min(10, N - i)
+        pool[i:i + k] = CONTENT[content](W, H, i, k, dev, full_range=FULL)
+    torch.cuda.synchronize()
+    for name in names:
+        _lib._lib = None
+        _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
+        from ffmpeg_distributed_amd.encoder import MjpegEncoder
+        enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, huffman="default",
+                           dct_mfma=False)
+        L = _lib.lib()
+        L.mjg_probe_phase.argtypes = [C.POINTER(C.c_ulonglong)]
+        acc = (C.c_ulonglong * 8)()
+        enc.submit(device_ptr=pool.data_ptr(), nframes=N)  # warm
+        enc.sync()
+        L.mjg_probe_phase(acc)
+        runs = 3
+        for _ in range(runs):
+            enc.submit(device_ptr=pool.data_ptr(), nframes=N)
+            enc.sync()
+        L.mjg_probe_phase(acc)
+        nchunks = -(-((W + 15) // 16) * ((H + 15) // 16) * 6 // 64) * N * runs  # 4:2:0 chunks per frame
+        tot = sum(acc)
+        print(f"== {name} {os.environ.get('WL', 'c2')} {content}: {tot / nchunks:.0f} cycles per chunk-wave "
+              f"({nchunks} chunk-waves)")
+        for i, p in enumerate(PHASES):
+            print(f"  {p:36s} {acc[i] / nchunks:8.0f}  {100 * acc[i] / max(tot, 1):5.1f}%")
+        enc.close()
+
+
+if __name__ == "__main__":
+    main()

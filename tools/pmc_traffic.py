@@ -46,6 +46,10 @@ def main():
     per_write = {4: cal_bytes / calw["k_calib_write4"]["WRITE_SIZE"],
                  1: cal_bytes / calw["k_calib_write1"]["WRITE_SIZE"]}
     import bench
+    from ffmpeg_distributed_amd import build as B
+    if not B.check():  # the counters describe the library the workload loaded: it must be HEAD's
+        raise SystemExit("libmjgpu.so is stale against its sources: rebuild before counting")
+    digest = B.source_digest()
     for wl in wls:
         W, H, DW, DH, Q, SEG, FULL, HUFF, text = bench.WORKLOADS[wl]
         # per launch = per submit of one segment (the workload syncs LAUNCHES submits); a
@@ -64,7 +68,8 @@ def main():
                              "write_bytes_per_launch": wv * per_write[ww],
                              "hbm_bytes_per_launch": f * per_read[rw] + wv * per_write[ww]}
         in_bytes = SEG * (W * H + 2 * ((W + 1) // 2) * ((H + 1) // 2))
-        res = {"workload": {"name": wl, "text": text, "frames_per_launch": SEG, "width": W, "height": H,
+        res = {"library_digest": digest,  # build.source_digest() of the counted library
+               "workload": {"name": wl, "text": text, "frames_per_launch": SEG, "width": W, "height": H,
                             "dst_width": DW, "dst_height": DH, "qscale": Q, "huffman": HUFF,
                             "input": "testsrc2-like (tools/pmc_workload.py)"},
                "calibration": {"kernel": "tools/calib_fetch.hip", "bytes": cal_bytes,

@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
 """Perf A/B of k_encode source variants in ONE process, interleaved rounds (guide §5.4
-rule 24).  VARIANTS="name=srcdir:flags;..." where srcdir holds api.hip & friends
-(default: the working tree) and flags are extra hipcc -D options.  Only kernel times
-are compared; run tests/test_gpu_parity.py for correctness of the shipped build."""
+rule 24).  VARIANTS="name=src:flags;..." where src is a directory holding api.hip & friends
+(default: the working tree) or `@patches` (tools/patches.py: the product source with the
+named experiment patches applied, e.g. `@no_skip+wide_cost=3`), and flags are extra hipcc
+options.  Only kernel times are compared; run tests/test_gpu_parity.py for correctness of
+the shipped build."""
 import os
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
 
 
@@ -17,12 +20,19 @@ def parse():
     for item in os.environ.get("VARIANTS", "cur=:").split(";"):
         name, rest = item.split("=", 1)
         src, _, flags = rest.partition(":")
-        out.append((name, os.path.abspath(os.path.join(ROOT, src)) if src else CSRC, flags.split()))
+        if src.startswith("@"):
+            src = os.path.join("tools", f"_v{name}src"), src[1:]
+        out.append((name, src, flags.split()))
     return out
 
 
 def build(name, src, flags):
     so = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
+    if isinstance(src, tuple):  # (copy dir, patch spec)
+        import patches
+        src = patches.apply(src[1], os.path.join(ROOT, src[0]))
+    else:
+        src = os.path.abspath(os.path.join(ROOT, src)) if src else CSRC
     from ffmpeg_distributed_amd import build as B  # the product's compile flags
     base = [a for a in B._command(so) if not a.endswith((".hip", ".cpp"))]
     cmd = base[:1] + [*flags] + base[1:] + [os.path.join(src, "api.hip"), os.path.join(CSRC, "sws_filter.cpp")]
