@@ -66,15 +66,6 @@ __device__ __forceinline__ uint32_t pass2_pair(int i) {  // int16 pair of entrie
   const int r = i >> 2, f = (r & 3) == 0 ? kPass2DcScale : 1;
   return (uint32_t)(uint16_t)(kPass2Dot[2 * i] * f) | ((uint32_t)(uint16_t)(kPass2Dot[2 * i + 1] * f) << 16);
 }
-// k_encode screen bit -> zigzag scan position.  Columns 0-3 (DC excluded) are shifted
-// into word A in the order col-major (col, row), columns 4-7 into word B, so the j-th
-// coefficient screened lands at bit 30-j (A) / 31-j (B).
-__device__ static constexpr uint8_t kScreenScatter[64] = {
-    49, 47, 38, 32, 24, 17, 13, 6, 48, 37, 33, 23, 18, 12, 7, 5,
-    36, 34, 22, 19, 11, 8, 4, 1, 35, 21, 20, 10, 9, 3, 2, 0,
-    63, 61, 60, 54, 53, 43, 42, 28, 62, 59, 55, 52, 44, 41, 29, 27,
-    58, 56, 51, 45, 40, 30, 26, 15, 57, 50, 46, 39, 31, 25, 16, 14};
-
 // Frame geometry.  A frame is a raster of MCUs of `bpm` blocks each (4:2:0: 16x16, Y0-3 Cb
 // Cr; 4:2:2: 16x16, Y0-3 Cb0 Cb1 Cr0 Cr1; 4:4:4: 8x16, Y0 Y1 Cb0 Cb1 Cr0 Cr1 -- FFmpeg's
 // coding order, see oracle/mjpeg_oracle.c or_layouts), split into `nseg` entropy-coded
@@ -489,25 +480,13 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
 
 // -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
 // (layout of the table block: AC luma 0-255, AC chroma 256-511, DC luma 512-527,
-// DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.
-// It also records every symbol with its mantissa in the lane's record column (rec[j * 64]:
-// DC flag << 31 | (DC category or AC symbol) << 16 | mantissa), so the emission pass
-// replays the symbols (k_emit_syms) instead of recomputing the block.
-constexpr int kSymCap = 68;  // symbols per block: DC + 63 AC + 3 ZRL + EOB
+// DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.  Nothing
+// else is kept: the emission pass (k_encode<.., kEmitOptimal>) encodes the frame again with the
+// frame's tables (k_huff_build).
 struct CountSink {
   uint32_t *hac, *hdc;
-  uint32_t *rec;
-  uint32_t n = 0;
-  __device__ __forceinline__ void dc(int cat, uint32_t mant) {
-    atomicAdd(&hdc[cat], 1u);
-    rec[n * 64] = (1u << 31) | ((uint32_t)cat << 16) | mant;
-    n++;
-  }
-  __device__ __forceinline__ void ac(int sym, int, uint32_t mant) {
-    atomicAdd(&hac[sym], 1u);
-    rec[n * 64] = ((uint32_t)sym << 16) | mant;
-    n++;
-  }
+  __device__ __forceinline__ void dc(int cat, uint32_t) { atomicAdd(&hdc[cat], 1u); }
+  __device__ __forceinline__ void ac(int sym, int, uint32_t) { atomicAdd(&hac[sym], 1u); }
   __device__ __forceinline__ void finish() {}
 };
 
@@ -666,9 +645,9 @@ __device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, boo
 }
 
 // MODE: kEmitDefault (-huffman default, Annex K tables), kCount (-huffman optimal pass 1:
-// per-frame symbol histograms into hist[frame][544] and each block's symbol records, which
-// k_emit_syms replays with the frame's own tables).
-constexpr int kEmitDefault = 0, kCount = 1;
+// per-frame symbol histograms into hist[frame][544]), kEmitOptimal (-huffman optimal pass 2:
+// the same encode with the frame's own tables, ftabs[frame][544] from k_huff_build).
+constexpr int kEmitDefault = 0, kCount = 1, kEmitOptimal = 2;
 constexpr int kFrameTabWords = 544;  // AC luma, AC chroma, DC luma, DC chroma (table block layout)
 
 // Pack a chunk's 64 block codes into its slot: a wave prefix-scan of the block lengths gives
@@ -830,8 +809,11 @@ __device__ __forceinline__ void row_pass(const uint64_t (&raw)[8], int tab, cons
 // jp's test skipped a column on the wave's previous test of it.  A pair is tested when it did,
 // or on every fourth chunk (retest); a pair whose columns are rarely skippable (detailed
 // content) then costs its test a quarter of the time (the test is ~20 VALU per pair).
+// The candidate bits are deposited straight at their zigzag positions (mlo: scan positions 0-31,
+// mhi: 32-63; r and col are compile-time after unrolling, so each bit costs a shift and an
+// and-or): the emission visits candidates in scan order with no scatter step.
 __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, const uint32_t *s_skip,
-                                              const float *s_thr, int &dc, uint32_t &ca, uint32_t &cb,
+                                              const float *s_thr, int &dc, uint32_t &mlo, uint32_t &mhi,
                                               uint32_t &st, bool retest) {
 #pragma unroll
   for (int jp = 0; jp < 4; jp++) {
@@ -873,13 +855,7 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
     for (int h = 0; h < 2; h++) {
       __builtin_amdgcn_sched_barrier(0);  // one column at a time
       const int col = 2 * jp + h;
-      if (h ? skip1 : skip0) {  // wave-uniform: 8 zero screen bits
-        if (col < 4)
-          ca <<= 8;
-        else
-          cb <<= 8;
-        continue;
-      }
+      if (h ? skip1 : skip0) continue;  // wave-uniform: no candidates in this column
       float x[8];
 #pragma unroll
       for (int r = 0; r < 8; r++)
@@ -908,33 +884,17 @@ __device__ __forceinline__ void column_screen(const uint32_t *s_pk, int lane, co
         if (col == 0 && r == 0) {
           dc = (int)(__float_as_uint(__builtin_fmaf(sv[0], 1.0f / 1024, 0x1.1p-7f) + kM) - 0x4B400000u);
         } else {
-          // sign of B^2 - s^2 shifted into the candidate word in computation order
-          // (v_alignbit: (m << 1) | (neg >> 31)); zigzag order is restored below
+          // the sign of B^2 - s^2 at the coefficient's scan position
           const uint32_t neg = __float_as_uint(__builtin_fmaf(-sv[r], sv[r], thr[r]));
-          if (col < 4)
-            ca = __builtin_amdgcn_alignbit(ca, neg, 31);
+          const int z = kZigzagInv[r * 8 + col];
+          if (z < 32)
+            mlo |= (neg >> 31) << z;
           else
-            cb = __builtin_amdgcn_alignbit(cb, neg, 31);
+            mhi |= (neg >> 31) << (z - 32);
         }
       }
     }
   }
-}
-
-// Candidate bits (column_screen) -> zigzag-ordered candidate mask (a handful per block).
-// One bit of each word per step, both table reads in flight together (one LDS round trip per
-// step, max(|A|, |B|) steps).  A word with no bit left reads a dummy entry: A's bit 31 is
-// never set (31 coefficients) and B's dummy is entry 64; both map to zigzag 0, the DC, which
-// is no candidate and is cleared at the end.
-__device__ __forceinline__ uint64_t screen_mask(uint32_t ca, uint32_t cb, const uint8_t *s_scat) {
-  uint64_t mask = 0;
-  while (ca | cb) {
-    const uint32_t pa = (uint32_t)__builtin_ctzg(ca, 31), pb = (uint32_t)__builtin_ctzg(cb, 32);
-    ca &= ca - 1;
-    cb &= cb - 1;
-    mask |= (1ull << s_scat[pa]) | (1ull << s_scat[32 + pb]);
-  }
-  return mask & ~1ull;
 }
 
 // DC predictor of this lane's block (FFmpeg last_dc, 128 at every segment start): the block
@@ -1149,30 +1109,32 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
-    uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all,
-    uint32_t *__restrict__ syms, uint32_t *__restrict__ symn) {
-  __shared__ uint32_t s_ac[512];
-  __shared__ uint32_t s_dc[32];
+    uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all) {
+  // hist: kCount the per-frame histograms (written), kEmitOptimal the per-frame code tables (read)
+  constexpr bool EMIT = MODE != kCount;
+  __shared__ uint32_t s_ac[MODE == kEmitDefault ? 512 : 1];  // Annex K codes (len << 16 | code)
+  __shared__ uint32_t s_dc[MODE == kEmitDefault ? 32 : 1];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ uint4 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
   constexpr bool SCR = !MF;  // the VALU column screen
   __shared__ __attribute__((aligned(16))) float s_thr[SCR ? 64 : 4];  // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
-  __shared__ uint8_t s_scat[SCR ? 68 : 4];  // candidate bit -> zigzag index (kScreenScatter; [64]: dummy)
   __shared__ uint8_t s_rc[RC ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
   __shared__ uint4 s_f[MF ? 12 * 64 : 1];  // MFMA A fragments (dct_mfma): [0, 2) pass 1, [4, 12) pass 2
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
   __shared__ uint4 s_bd[16];                       // their plane fields (BlockDesc)
   __shared__ uint32_t s_skip[SCR ? 12 : 1];        // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
-  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
-  // per wave: the current frame's histogram (kCount)
+  __shared__ uint32_t s_hv_all[EMIT ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
+  // per wave: the current frame's histogram (kCount) or code tables (kEmitOptimal)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][MODE == kEmitDefault ? 1 : kFrameTabWords];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
-  if (tid < 32) s_dc[tid] = tabs[512 + tid];
+  if (MODE == kEmitDefault) {
+    for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
+    if (tid < 32) s_dc[tid] = tabs[512 + tid];
+  }
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
@@ -1180,8 +1142,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     if (SCR) s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
       s_m2[tid] = pass2_pair(tid);
-    if (SCR) s_scat[tid] = kScreenScatter[tid];
-    if (SCR && tid < 4) s_scat[64 + tid] = 0;
   }
   if (tid < 8) {
     s_desc[tid] = tabs[672 + tid];
@@ -1194,19 +1154,22 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
   uint32_t *s_pk = s_pk_all[wave];
-  uint32_t *s_hv = s_hv_all[MODE == kEmitDefault ? wave : 0];
-  if (MODE == kEmitDefault)
+  uint32_t *s_hv = s_hv_all[EMIT ? wave : 0];
+  if (EMIT)
     for (int i = lane; i < kStageWords; i += 64) s_hv[i] = 0u;
   uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
   if (MODE == kCount)
     for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
   int aux_frame = -1;  // frame whose histogram / tables s_aux holds (wave-uniform)
+  // the code tables the emission uses: Annex K, or (kEmitOptimal) the wave's frame's own
+  const uint32_t *const tac = MODE == kEmitOptimal ? s_aux : s_ac;
+  const uint32_t *const tdc = MODE == kEmitOptimal ? s_aux + 512 : s_dc;
   __syncthreads();  // tables visible; the only workgroup barrier
 
   const int gw = blockIdx.x * kWavesPerWg + wave;
   constexpr int kBatch = kBatchOf<MF>;
   const int nbatch = (ntasks + kBatch - 1) / kBatch;
-  constexpr int NX = MODE == kEmitDefault ? kXcds : 1;
+  constexpr int NX = EMIT ? kXcds : 1;
   const XcdUnits<NX> xu{(int)(blockIdx.x & (NX - 1)), nbatch};
   const int nwg = gridDim.x;
   int u0 = xu.start(xu.j) + (int)(blockIdx.x / NX) * kWavesPerWg + wave;  // static first unit
@@ -1269,9 +1232,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     // a new batch starts at an arbitrary chunk: fetch its predecessors' rows now
     const uint64_t crow = (new_batch && tn >= 0) ? carry_row(fb, g, bbase, chunk, lane, s_bd) : 0;
 
-    uint32_t ca = 0, cb = 0;  // screen bits, columns 0-3 (31 AC) and 4-7 (32), see below
+    uint32_t mlo = 0, mhi = 0;  // candidate mask, scan positions 0-31 / 32-63 (column_screen)
     if (cur_active) {
-      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, ca, cb, skip_st, (t & 3) == 0);
+      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, mlo, mhi, skip_st, (t & 3) == 0);
       if (DBG && g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
@@ -1283,7 +1246,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
         }
       }
     }
-    if (SCR) mask = screen_mask(ca, cb, s_scat);
+    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;
 
     // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.
@@ -1301,10 +1264,15 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       aux_frame = cur_frame;
     }
+    if (MODE == kEmitOptimal && cur_frame != aux_frame) {  // the frame's code tables
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's reads of the old ones are done
+      for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = hist[(size_t)cur_frame * kFrameTabWords + i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      aux_frame = cur_frame;
+    }
     if (MODE == kCount) {
-      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kSymCap * 64 + lane};
+      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16};
       if (cur_active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
-      symn[(size_t)t * 64 + lane] = cs.n;
       if (tn < 0) break;
       if (new_batch) {
         carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
@@ -1314,8 +1282,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       continue;
     }
     ShiftSink q;
-    q.act = s_ac + tab * 256;
-    q.dct = s_dc + tab * 16;
+    q.act = tac + tab * 256;
+    q.dct = tdc + tab * 16;
     uint32_t *stage_w = stage_all + (size_t)gw * 64 * kStageWords;
     q.stage = stage_w + lane;
     const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);
@@ -1327,7 +1295,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       for (uint64_t hw = wide; hw; hw &= hw - 1) {
         const int h = (int)__builtin_ctzll(hw);
         const uint32_t nb = emit_block_wave(s_pk, h, __builtin_amdgcn_readlane(diff, h),
-                                            __builtin_amdgcn_readlane(tab, h), s_zd, s_m2, s_ac, s_dc,
+                                            __builtin_amdgcn_readlane(tab, h), s_zd, s_m2, tac, tdc,
                                             s_hv, stage_w, lane);
         if (lane == h) {
           q.bits = nb;
@@ -1350,76 +1318,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       const uint32_t v = s_aux[i];
       if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
     }
-  }
-}
-
-// ------------------------------------------------------------ k_emit_syms
-// -huffman optimal, emission pass: every block's symbols as the counting pass recorded
-// them (CountSink), coded with the frame's tables (k_huff_build) and packed as k_encode
-// packs them.  No pixels, no DCT: one wave per chunk, lane = block; the record words are
-// loaded 8 per step (4: 2.5% slower on c1).  Persistent waves (the long-block staging columns are per wave).
-__global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
-    EncGeom g, const uint32_t *__restrict__ tabs, const uint32_t *__restrict__ ftabs,
-    const uint32_t *__restrict__ syms, const uint32_t *__restrict__ symn, uint32_t *__restrict__ scratch,
-    uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ stage_all, int ntasks) {
-  __shared__ uint32_t s_aux_all[kWavesPerWg][kFrameTabWords];
-  __shared__ uint32_t s_desc[8];
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  if (tid < 8) s_desc[tid] = tabs[672 + tid];
-  __syncthreads();
-  uint32_t *s_aux = s_aux_all[wave];
-  const int nwaves = gridDim.x * kWavesPerWg, gw = blockIdx.x * kWavesPerWg + wave;
-  int aux_frame = -1;
-  // the chunk's symbol count and first 8 records are loaded one chunk ahead (the records
-  // past a block's count are never used, and every one of them is inside the record array)
-  uint32_t n_nx = 0, e_nx[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-  auto head = [&](int tt) {
-    int frame, chunk, bbase;
-    task_pos(g, tt, frame, chunk, bbase);
-    const int b = chunk * 64 + lane;
-    n_nx = b < g.seg_blocks ? symn[(size_t)tt * 64 + lane] : 0u;
-    const uint32_t *rec = syms + (size_t)tt * kSymCap * 64 + lane;
-#pragma unroll
-    for (int i = 0; i < 8; i++) e_nx[i] = rec[i * 64];
-  };
-  if (gw < ntasks) head(gw);
-  for (int t = gw; t < ntasks; t += nwaves) {
-    int frame, chunk, bbase;
-    task_pos(g, t, frame, chunk, bbase);
-    const uint32_t n = n_nx;
-    uint32_t e[8] = {e_nx[0], e_nx[1], e_nx[2], e_nx[3], e_nx[4], e_nx[5], e_nx[6], e_nx[7]};
-    if (t + nwaves < ntasks) head(t + nwaves);
-    if (frame != aux_frame) {  // the frame's code tables into the wave's LDS
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = ftabs[(size_t)frame * kFrameTabWords + i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      aux_frame = frame;
-    }
-    const int b = chunk * 64 + lane;
-    const bool active = b < g.seg_blocks;
-    const int tab = desc_tab(s_desc[block_in_mcu(g, b)]);
-    ShiftSink q;
-    q.act = s_aux + tab * 256;
-    q.dct = s_aux + 512 + tab * 16;
-    q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
-    const uint32_t *rec = syms + (size_t)t * kSymCap * 64 + lane;
-    for (uint32_t j0 = 0; j0 < n; j0 += 8) {
-      if (j0) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) e[i] = j0 + i < n ? rec[(j0 + i) * 64] : 0u;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        if (j0 + i >= n) break;
-        const uint32_t v = (e[i] >> 16) & 0xffu, mant = e[i] & 0xffffu;
-        if (e[i] >> 31)
-          q.dc((int)v, mant);
-        else
-          q.ac((int)v, (int)(v & 15u), mant);
-      }
-    }
-    q.finish();
-    pack_chunk(q, active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
   }
 }
 

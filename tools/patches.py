@@ -74,8 +74,8 @@ PATCHES = {
     B[i] = nB ? B[i] : 0u;
 """)],
     # occupancy probe: k_encode's workgroup LDS past 40 KB (3 workgroups, 3 waves per SIMD)
-    "occ3": lambda a: [(K, "  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];",
-                        "  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords + 512];")],
+    "occ3": lambda a: [(K, "  __shared__ uint32_t s_hv_all[EMIT ? kWavesPerWg : 1][kStageWords];",
+                        "  __shared__ uint32_t s_hv_all[EMIT ? kWavesPerWg : 1][kStageWords + 512];")],
 }
 
 # ---------------------------------------------------------------- probes (wrong timing, right bytes)
@@ -98,8 +98,8 @@ def _phase_clock(a):
          "  unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_prev = __builtin_amdgcn_s_memtime();\n"
          "  while (true) {\n    MJG_PH(7);\n    // the next unit is reserved"),
         (K, "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);\n", "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);\n    MJG_PH(0);\n"),
-        (K, "    uint32_t ca = 0, cb = 0;  // screen bits", "    MJG_PH(1);\n    uint32_t ca = 0, cb = 0;  // screen bits"),
-        (K, "    if (SCR) mask = screen_mask(ca, cb, s_scat);\n", "    if (SCR) mask = screen_mask(ca, cb, s_scat);\n    MJG_PH(2);\n"),
+        (K, "    uint32_t mlo = 0, mhi = 0;  // candidate mask", "    MJG_PH(1);\n    uint32_t mlo = 0, mhi = 0;  // candidate mask"),
+        (K, "    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;\n", "    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;\n    MJG_PH(2);\n"),
         (K, "    if (cur_active && !((wide >> lane) & 1ull)) {", "    MJG_PH(3);\n    if (cur_active && !((wide >> lane) & 1ull)) {"),
         (K, "    if (wide) {  // the heavy blocks", "    MJG_PH(4);\n    if (wide) {  // the heavy blocks"),
         (K, "    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    if (tn < 0) break;",

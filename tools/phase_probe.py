@@ -37,7 +37,7 @@ def main():
         from ffmpeg_distributed_amd.encoder import MjpegEncoder
         enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, huffman="default",
                            dct_mfma=False)
-        L = _lib.lib()
+        L = _lib.load()
         L.mjg_probe_phase.argtypes = [C.POINTER(C.c_ulonglong)]
         acc = (C.c_ulonglong * 8)()
         enc.submit(device_ptr=pool.data_ptr(), nframes=N)  # warm
