@@ -191,6 +191,7 @@ struct Slot {
   uint8_t *d_out = nullptr;
   size_t out_cap = 0;
   uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_dht_nval = nullptr, *d_hdr_lens = nullptr;  // optimal
+  uint32_t *d_syms = nullptr, *d_symn = nullptr;  // optimal: per block, the symbols the counting pass saw
   uint8_t *d_dht = nullptr;
   int16_t *d_dbg = nullptr;
   uint64_t *h_sizes = nullptr;
@@ -211,7 +212,7 @@ struct mjg_ctx {
   EncGeom geom{};
   int32_t qmat[64];
   int enc_grid = 0;             // persistent k_encode workgroups: every CU full (kEmitDefault)
-  int enc_grid_cnt = 0, enc_grid_opt = 0;  // the same for the -huffman optimal passes (kCount, kEmitOptimal)
+  int enc_grid_cnt = 0;         // the same for the -huffman optimal counting pass (kCount: more LDS)
   bool scale = false;
   size_t in_frame_bytes = 0, enc_frame_bytes = 0;
   std::vector<uint8_t> hdr;
@@ -219,7 +220,7 @@ struct mjg_ctx {
 
   uint32_t *d_tabs = nullptr;
   uint8_t *d_hdr = nullptr;
-  size_t stage_cols = 0;       // staging columns per slot (persistent waves of k_encode / fused)
+  size_t stage_cols = 0;       // staging columns per slot (persistent waves of k_encode / k_emit_syms / fused)
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
@@ -260,7 +261,7 @@ void free_ctx(mjg_ctx *c) {
   for (Slot &S : c->slot) {
     void *sp[] = {S.d_stage, S.d_scaled, S.d_stage_bits, S.d_scratch, S.d_stream, S.d_work, S.d_chunk_bits, S.d_chunk_off, S.d_group_ff, S.d_ff_off, S.d_frame_bits,
                   S.d_status, S.d_frame_size, S.d_frame_offsets, S.d_seg_size, S.d_seg_off, S.d_done, S.d_out,
-                  S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg};
+                  S.d_hist, S.d_ftabs, S.d_dht_nval, S.d_hdr_lens, S.d_dht, S.d_dbg, S.d_syms, S.d_symn};
     for (void *p : sp)
       if (p) (void)hipFree(p);
     if (S.h_sizes) (void)hipHostFree(S.h_sizes);
@@ -428,7 +429,8 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   if (c->optimal &&
       ((rc = dmalloc(&S.d_hist, B * kFrameTabWords)) || (rc = dmalloc(&S.d_ftabs, B * kFrameTabWords)) ||
        (rc = dmalloc(&S.d_dht, B * 4 * kDhtSlot)) || (rc = dmalloc(&S.d_dht_nval, B * 4)) ||
-       (rc = dmalloc(&S.d_hdr_lens, B))))
+       (rc = dmalloc(&S.d_hdr_lens, B)) || (rc = dmalloc(&S.d_syms, B * NC * (size_t)kSymCap * 64)) ||
+       (rc = dmalloc(&S.d_symn, B * NC * 64))))
     return rc;
   if (g.debug_coefs && (rc = dmalloc(&S.d_dbg, B * (size_t)g.nmcu * g.bpm * 64))) return rc;
   HIP_TRY(hipHostMalloc((void **)&S.h_sizes, (B + 1) * sizeof(uint64_t), hipHostMallocDefault));
@@ -779,20 +781,17 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       &per_cu, c->dct_mfma ? (const void *)k_encode<true, kEmitDefault, true> : (const void *)k_encode<true, kEmitDefault>,
       64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
-  c->enc_grid_cnt = c->enc_grid_opt = c->enc_grid;
-  if (c->optimal) {  // more LDS per workgroup (the per-wave histograms / code tables): fewer fit
-    int pc = 0, po = 0;
+  c->enc_grid_cnt = c->enc_grid;
+  if (c->optimal) {  // the per-wave histograms: fewer workgroups per CU (3 instead of 4)
+    int pc = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void *)k_encode<true, kCount>, 64 * kWavesPerWg, 0));
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&po, (const void *)k_encode<true, kEmitOptimal>,
-                                                         64 * kWavesPerWg, 0));
     c->enc_grid_cnt = std::max(1, ncu * std::max(1, pc));
-    c->enc_grid_opt = std::max(1, ncu * std::max(1, po));
   }
-  size_t stage_cols = (size_t)std::max(c->enc_grid, c->enc_grid_opt) * kWavesPerWg;
+  size_t stage_cols = (size_t)c->enc_grid * kWavesPerWg;
   if (c->fused) {
     int fper = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &fper, c->optimal ? (const void *)k_scale_encode<8, 5, true, kEmitOptimal> : (const void *)k_scale_encode<8, 5, true, kEmitDefault>,
+        &fper, c->optimal ? (const void *)k_scale_encode<8, 5, true, kCount> : (const void *)k_scale_encode<8, 5, true, kEmitDefault>,
         64 * kFusedWaves, 0));
     c->fused_grid = std::max(1, ncu * std::max(1, fper));
     stage_cols = std::max(stage_cols, (size_t)c->fused_grid * kFusedWaves);
@@ -837,7 +836,7 @@ void launch_fused3(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
   k_scale_encode<HT, NPV, RANGE_ON, MODE><<<c->fused_grid, 64 * kFusedWaves, 0, S.st>>>(
       src, c->geom, c->fgeom, c->d_tabs, (const uint32_t *)c->ps[0].d_fh, (const uint32_t *)c->ps[0].d_fv,
       (const uint32_t *)c->ps[1].d_fh, (const uint32_t *)c->ps[1].d_fv, S.d_scratch, S.d_chunk_bits,
-      S.d_stage_bits, S.d_work, n, MODE == kEmitOptimal ? S.d_ftabs : S.d_hist);
+      S.d_stage_bits, S.d_work, n, S.d_hist, S.d_syms, S.d_symn);
 }
 
 template <int MODE>
@@ -852,24 +851,22 @@ void launch_fused(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
 template <int MODE, bool MF, bool DBG>
 void launch_encode3(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
-  uint32_t *tabs = MODE == kEmitOptimal ? S.d_ftabs : S.d_hist;  // see k_encode's `hist`
   if (g.range_convert)
     k_encode<true, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
-        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, tabs, S.d_stage_bits);
+        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
+        S.d_stage_bits, S.d_syms, S.d_symn);
   else
     k_encode<false, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
-        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, tabs, S.d_stage_bits);
+        enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
+        S.d_stage_bits, S.d_syms, S.d_symn);
 }
 
 template <int MODE, bool MF>
 void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
-  if constexpr (MODE != kEmitOptimal) {  // (optimal: the counting pass writes them)
-    if (c->geom.debug_coefs) {
-      launch_encode3<MODE, MF, true>(c, S, enc_in, wgs, ntasks);
-      return;
-    }
-  }
-  launch_encode3<MODE, MF, false>(c, S, enc_in, wgs, ntasks);
+  if (c->geom.debug_coefs)
+    launch_encode3<MODE, MF, true>(c, S, enc_in, wgs, ntasks);
+  else
+    launch_encode3<MODE, MF, false>(c, S, enc_in, wgs, ntasks);
 }
 
 // The DCT stage: the VALU passes, or (-huffman default) dct_mfma.
@@ -1032,10 +1029,10 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     HIP_TRY(hipGetLastError());
   }
   tmark(c, S, MJG_K_ENCODE, 0);
-  if (c->optimal && c->fused)
-    launch_fused<kEmitOptimal>(c, S, src, n);
-  else if (c->optimal)
-    launch_encode<kEmitOptimal>(c, S, enc_in, std::min(wgs, c->enc_grid_opt), ntasks);
+  if (c->optimal)
+    k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, S.st>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
+                                                             S.d_scratch, S.d_chunk_bits, S.d_stage_bits,
+                                                                  ntasks);
   else if (c->fused)
     launch_fused<kEmitDefault>(c, S, src, n);
   else

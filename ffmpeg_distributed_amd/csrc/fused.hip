@@ -297,10 +297,10 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
     const uint32_t *__restrict__ htab0, const uint32_t *__restrict__ vtab0,
     const uint32_t *__restrict__ htab1, const uint32_t *__restrict__ vtab1,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ stage_all,
-    uint32_t *__restrict__ work_ctr, int nframes, uint32_t *__restrict__ hist) {
-  // hist: kCount the per-frame histograms (written), kEmitOptimal the per-frame code tables (read)
-  __shared__ uint32_t s_ac[MODE == kEmitDefault ? 512 : 1];
-  __shared__ uint32_t s_dc[MODE == kEmitDefault ? 32 : 1];
+    uint32_t *__restrict__ work_ctr, int nframes, uint32_t *__restrict__ hist, uint32_t *__restrict__ syms,
+    uint32_t *__restrict__ symn) {
+  __shared__ uint32_t s_ac[512];
+  __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];
   __shared__ uint8_t s_zz[64];
   __shared__ uint4 s_zd[64];  // zigzag -> exact_coef descriptor (zz_desc)
@@ -314,10 +314,8 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kFusedWaves][kFrameTabWords];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  if (MODE == kEmitDefault) {
-    for (int i = tid; i < 512; i += 64 * kFusedWaves) s_ac[i] = tabs[i];
-    if (tid < 32) s_dc[tid] = tabs[512 + tid];
-  }
+  for (int i = tid; i < 512; i += 64 * kFusedWaves) s_ac[i] = tabs[i];
+  if (tid < 32) s_dc[tid] = tabs[512 + tid];
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
@@ -339,9 +337,7 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
   const int runs_pf = (fg.gpf + fg.groups_per_wg - 1) / fg.groups_per_wg;
   const int nunits = runs_pf * nframes;
   uint32_t *stage = stage_all + ((size_t)blockIdx.x * kFusedWaves + wave) * 64 * kStageWords + lane;
-  int aux_frame = -1;  // frame whose histogram / code tables s_aux holds
-  const uint32_t *const tac = MODE == kEmitOptimal ? s_aux : s_ac;
-  const uint32_t *const tdc = MODE == kEmitOptimal ? s_aux + 512 : s_dc;
+  int aux_frame = -1;  // frame whose histogram s_aux holds (kCount)
 
   // Persistent workgroups: unit = (frame, run of groups_per_wg consecutive groups); the first
   // unit is blockIdx.x, the next ones come from work_ctr (zeroed by the tail's scan kernel).
@@ -394,12 +390,6 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       aux_frame = frame;
     }
-    if (MODE == kEmitOptimal && frame != aux_frame) {  // the frame's code tables
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = hist[(size_t)frame * kFrameTabWords + i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      aux_frame = frame;
-    }
 
     for (int grp = g0; grp < g1; grp++) {
       // phase 1: the group's scaled pixels into the LDS image
@@ -436,12 +426,13 @@ __global__ __launch_bounds__(64 * kFusedWaves, 4) void k_scale_encode(
       const int diff = dc - dc_predictor(dc, carry, desc_delta(dsc), chunk == 0, lane);
       const size_t t = (size_t)frame * g.nchunks + chunk;
       if (MODE == kCount) {
-        CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16};
+        CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + t * kSymCap * 64 + lane};
         if (active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
+        if (chunk < g.nchunks) symn[t * 64 + lane] = cs.n;
       } else {
         ShiftSink q;
-        q.act = tac + tab * 256;
-        q.dct = tdc + tab * 16;
+        q.act = s_ac + tab * 256;
+        q.dct = s_dc + tab * 16;
         q.stage = stage;
         if (active) {
           emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);

@@ -480,13 +480,25 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
 
 // -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
 // (layout of the table block: AC luma 0-255, AC chroma 256-511, DC luma 512-527,
-// DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.  Nothing
-// else is kept: the emission pass (k_encode<.., kEmitOptimal>) encodes the frame again with the
-// frame's tables (k_huff_build).
+// DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.
+// It also records every symbol with its mantissa in the lane's record column (rec[j * 64]:
+// DC flag << 31 | (DC category or AC symbol) << 16 | mantissa), so the emission pass
+// replays the symbols (k_emit_syms) instead of recomputing the block.
+constexpr int kSymCap = 68;  // symbols per block: DC + 63 AC + 3 ZRL + EOB
 struct CountSink {
   uint32_t *hac, *hdc;
-  __device__ __forceinline__ void dc(int cat, uint32_t) { atomicAdd(&hdc[cat], 1u); }
-  __device__ __forceinline__ void ac(int sym, int, uint32_t) { atomicAdd(&hac[sym], 1u); }
+  uint32_t *rec;
+  uint32_t n = 0;
+  __device__ __forceinline__ void dc(int cat, uint32_t mant) {
+    atomicAdd(&hdc[cat], 1u);
+    rec[n * 64] = (1u << 31) | ((uint32_t)cat << 16) | mant;
+    n++;
+  }
+  __device__ __forceinline__ void ac(int sym, int, uint32_t mant) {
+    atomicAdd(&hac[sym], 1u);
+    rec[n * 64] = ((uint32_t)sym << 16) | mant;
+    n++;
+  }
   __device__ __forceinline__ void finish() {}
 };
 
@@ -645,9 +657,9 @@ __device__ __forceinline__ int carry_finish(uint64_t w, int chunk, int lane, boo
 }
 
 // MODE: kEmitDefault (-huffman default, Annex K tables), kCount (-huffman optimal pass 1:
-// per-frame symbol histograms into hist[frame][544]), kEmitOptimal (-huffman optimal pass 2:
-// the same encode with the frame's own tables, ftabs[frame][544] from k_huff_build).
-constexpr int kEmitDefault = 0, kCount = 1, kEmitOptimal = 2;
+// per-frame symbol histograms into hist[frame][544] and each block's symbol records, which
+// k_emit_syms replays with the frame's own tables).
+constexpr int kEmitDefault = 0, kCount = 1;
 constexpr int kFrameTabWords = 544;  // AC luma, AC chroma, DC luma, DC chroma (table block layout)
 
 // Pack a chunk's 64 block codes into its slot: a wave prefix-scan of the block lengths gives
@@ -1109,11 +1121,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
-    uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all) {
-  // hist: kCount the per-frame histograms (written), kEmitOptimal the per-frame code tables (read)
-  constexpr bool EMIT = MODE != kCount;
-  __shared__ uint32_t s_ac[MODE == kEmitDefault ? 512 : 1];  // Annex K codes (len << 16 | code)
-  __shared__ uint32_t s_dc[MODE == kEmitDefault ? 32 : 1];
+    uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all,
+    uint32_t *__restrict__ syms, uint32_t *__restrict__ symn) {
+  __shared__ uint32_t s_ac[512];
+  __shared__ uint32_t s_dc[32];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ uint4 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
@@ -1126,15 +1137,13 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint4 s_bd[16];                       // their plane fields (BlockDesc)
   __shared__ uint32_t s_skip[SCR ? 12 : 1];        // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
-  __shared__ uint32_t s_hv_all[EMIT ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
-  // per wave: the current frame's histogram (kCount) or code tables (kEmitOptimal)
+  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
+  // per wave: the current frame's histogram (kCount)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][MODE == kEmitDefault ? 1 : kFrameTabWords];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  if (MODE == kEmitDefault) {
-    for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
-    if (tid < 32) s_dc[tid] = tabs[512 + tid];
-  }
+  for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
+  if (tid < 32) s_dc[tid] = tabs[512 + tid];
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
@@ -1154,22 +1163,19 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
   uint32_t *s_pk = s_pk_all[wave];
-  uint32_t *s_hv = s_hv_all[EMIT ? wave : 0];
-  if (EMIT)
+  uint32_t *s_hv = s_hv_all[MODE == kEmitDefault ? wave : 0];
+  if (MODE == kEmitDefault)
     for (int i = lane; i < kStageWords; i += 64) s_hv[i] = 0u;
   uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
   if (MODE == kCount)
     for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
   int aux_frame = -1;  // frame whose histogram / tables s_aux holds (wave-uniform)
-  // the code tables the emission uses: Annex K, or (kEmitOptimal) the wave's frame's own
-  const uint32_t *const tac = MODE == kEmitOptimal ? s_aux : s_ac;
-  const uint32_t *const tdc = MODE == kEmitOptimal ? s_aux + 512 : s_dc;
   __syncthreads();  // tables visible; the only workgroup barrier
 
   const int gw = blockIdx.x * kWavesPerWg + wave;
   constexpr int kBatch = kBatchOf<MF>;
   const int nbatch = (ntasks + kBatch - 1) / kBatch;
-  constexpr int NX = EMIT ? kXcds : 1;
+  constexpr int NX = MODE == kEmitDefault ? kXcds : 1;
   const XcdUnits<NX> xu{(int)(blockIdx.x & (NX - 1)), nbatch};
   const int nwg = gridDim.x;
   int u0 = xu.start(xu.j) + (int)(blockIdx.x / NX) * kWavesPerWg + wave;  // static first unit
@@ -1264,15 +1270,10 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       aux_frame = cur_frame;
     }
-    if (MODE == kEmitOptimal && cur_frame != aux_frame) {  // the frame's code tables
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's reads of the old ones are done
-      for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = hist[(size_t)cur_frame * kFrameTabWords + i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      aux_frame = cur_frame;
-    }
     if (MODE == kCount) {
-      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16};
+      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kSymCap * 64 + lane};
       if (cur_active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
+      symn[(size_t)t * 64 + lane] = cs.n;
       if (tn < 0) break;
       if (new_batch) {
         carry = carry_finish(crow, chunk, lane, rc, g, s_desc);
@@ -1282,8 +1283,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       continue;
     }
     ShiftSink q;
-    q.act = tac + tab * 256;
-    q.dct = tdc + tab * 16;
+    q.act = s_ac + tab * 256;
+    q.dct = s_dc + tab * 16;
     uint32_t *stage_w = stage_all + (size_t)gw * 64 * kStageWords;
     q.stage = stage_w + lane;
     const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);
@@ -1295,7 +1296,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       for (uint64_t hw = wide; hw; hw &= hw - 1) {
         const int h = (int)__builtin_ctzll(hw);
         const uint32_t nb = emit_block_wave(s_pk, h, __builtin_amdgcn_readlane(diff, h),
-                                            __builtin_amdgcn_readlane(tab, h), s_zd, s_m2, tac, tdc,
+                                            __builtin_amdgcn_readlane(tab, h), s_zd, s_m2, s_ac, s_dc,
                                             s_hv, stage_w, lane);
         if (lane == h) {
           q.bits = nb;
@@ -1318,6 +1319,76 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       const uint32_t v = s_aux[i];
       if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
     }
+  }
+}
+
+// ------------------------------------------------------------ k_emit_syms
+// -huffman optimal, emission pass: every block's symbols as the counting pass recorded
+// them (CountSink), coded with the frame's tables (k_huff_build) and packed as k_encode
+// packs them.  No pixels, no DCT: one wave per chunk, lane = block; the record words are
+// loaded 8 per step (4: 2.5% slower on c1).  Persistent waves (the long-block staging columns are per wave).
+__global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
+    EncGeom g, const uint32_t *__restrict__ tabs, const uint32_t *__restrict__ ftabs,
+    const uint32_t *__restrict__ syms, const uint32_t *__restrict__ symn, uint32_t *__restrict__ scratch,
+    uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ stage_all, int ntasks) {
+  __shared__ uint32_t s_aux_all[kWavesPerWg][kFrameTabWords];
+  __shared__ uint32_t s_desc[8];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (tid < 8) s_desc[tid] = tabs[672 + tid];
+  __syncthreads();
+  uint32_t *s_aux = s_aux_all[wave];
+  const int nwaves = gridDim.x * kWavesPerWg, gw = blockIdx.x * kWavesPerWg + wave;
+  int aux_frame = -1;
+  // the chunk's symbol count and first 8 records are loaded one chunk ahead (the records
+  // past a block's count are never used, and every one of them is inside the record array)
+  uint32_t n_nx = 0, e_nx[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  auto head = [&](int tt) {
+    int frame, chunk, bbase;
+    task_pos(g, tt, frame, chunk, bbase);
+    const int b = chunk * 64 + lane;
+    n_nx = b < g.seg_blocks ? symn[(size_t)tt * 64 + lane] : 0u;
+    const uint32_t *rec = syms + (size_t)tt * kSymCap * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < 8; i++) e_nx[i] = rec[i * 64];
+  };
+  if (gw < ntasks) head(gw);
+  for (int t = gw; t < ntasks; t += nwaves) {
+    int frame, chunk, bbase;
+    task_pos(g, t, frame, chunk, bbase);
+    const uint32_t n = n_nx;
+    uint32_t e[8] = {e_nx[0], e_nx[1], e_nx[2], e_nx[3], e_nx[4], e_nx[5], e_nx[6], e_nx[7]};
+    if (t + nwaves < ntasks) head(t + nwaves);
+    if (frame != aux_frame) {  // the frame's code tables into the wave's LDS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = ftabs[(size_t)frame * kFrameTabWords + i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      aux_frame = frame;
+    }
+    const int b = chunk * 64 + lane;
+    const bool active = b < g.seg_blocks;
+    const int tab = desc_tab(s_desc[block_in_mcu(g, b)]);
+    ShiftSink q;
+    q.act = s_aux + tab * 256;
+    q.dct = s_aux + 512 + tab * 16;
+    q.stage = stage_all + (size_t)gw * 64 * kStageWords + lane;
+    const uint32_t *rec = syms + (size_t)t * kSymCap * 64 + lane;
+    for (uint32_t j0 = 0; j0 < n; j0 += 8) {
+      if (j0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) e[i] = j0 + i < n ? rec[(j0 + i) * 64] : 0u;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        if (j0 + i >= n) break;
+        const uint32_t v = (e[i] >> 16) & 0xffu, mant = e[i] & 0xffffu;
+        if (e[i] >> 31)
+          q.dc((int)v, mant);
+        else
+          q.ac((int)v, (int)(v & 15u), mant);
+      }
+    }
+    q.finish();
+    pack_chunk(q, active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
   }
 }
 

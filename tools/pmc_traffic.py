@@ -47,9 +47,14 @@ def main():
                  1: cal_bytes / calw["k_calib_write1"]["WRITE_SIZE"]}
     import bench
     from ffmpeg_distributed_amd import build as B
-    if not B.check():  # the counters describe the library the workload loaded: it must be HEAD's
-        raise SystemExit("libmjgpu.so is stale against its sources: rebuild before counting")
-    digest = B.source_digest()
+    if os.environ.get("MJG_LIBRARY"):  # a variant library (an A/B record): its file's digest
+        import hashlib
+        with open(os.environ["MJG_LIBRARY"], "rb") as f:
+            digest = "file:" + hashlib.sha256(f.read()).hexdigest()
+    else:
+        if not B.check():  # the counters describe the library the workload loaded: it must be HEAD's
+            raise SystemExit("libmjgpu.so is stale against its sources: rebuild before counting")
+        digest = B.source_digest()
     for wl in wls:
         W, H, DW, DH, Q, SEG, FULL, HUFF, text = bench.WORKLOADS[wl]
         # per launch = per submit of one segment (the workload syncs LAUNCHES submits); a
@@ -76,7 +81,10 @@ def main():
                                "fetch_bytes_per_unit": per_read, "write_bytes_per_unit": per_write},
                "input_plane_bytes_per_launch": in_bytes,
                "kernels": kernels}
-        for pth in (os.path.join(ROOT, "profiles", f"pmc_{wl}.json"), os.path.join(out, f"pmc_{wl}.json")):
+        dests = [os.path.join(out, f"pmc_{wl}.json")]
+        if not os.environ.get("MJG_LIBRARY"):
+            dests.append(os.path.join(ROOT, "profiles", f"pmc_{wl}.json"))
+        for pth in dests:
             with open(pth, "w") as fo:
                 json.dump(res, fo, indent=1)
         print(wl, json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 1) for k, v in kernels.items()}))
