@@ -74,8 +74,7 @@ PATCHES = {
     B[i] = nB ? B[i] : 0u;
 """)],
     # occupancy probe: k_encode's workgroup LDS past 40 KB (3 workgroups, 3 waves per SIMD)
-    "occ3": lambda a: [(K, "  __shared__ uint32_t s_hv_all[EMIT ? kWavesPerWg : 1][kStageWords];",
-                        "  __shared__ uint32_t s_hv_all[EMIT ? kWavesPerWg : 1][kStageWords + 512];")],
+    "occ3": lambda a: [(K, "][kStageWords];  // emit_block_wave", "][kStageWords + 512];  // emit_block_wave")],
 }
 
 # ---------------------------------------------------------------- probes (wrong timing, right bytes)
