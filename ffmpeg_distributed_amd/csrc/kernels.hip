@@ -200,6 +200,11 @@ __device__ __forceinline__ int wave_sum(int v) {
   __device__ __forceinline__ void ac(int sym, int cat, uint32_t mant) {               \
     const uint32_t e = act[sym];                                                      \
     emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);                        \
+  }                                                                                   \
+  /* the AC code of sym (a table read issued early), then its emission */             \
+  __device__ __forceinline__ uint32_t lookup(int sym) const { return act[sym]; }      \
+  __device__ __forceinline__ void put_ac(uint32_t e, int, int cat, uint32_t mant) {   \
+    emit(((e & 0xffffu) << cat) | mant, (int)(e >> 16) + cat);                        \
   }
 
 __device__ __forceinline__ int dc_cat(int diff) {
@@ -300,7 +305,7 @@ __device__ __forceinline__ int exact_coef(const uint32_t *pkcol, int n, const ui
 }
 
 // exact_coef for zigzag position k from its descriptor (zz_desc, in LDS), returned as
-// t = v - (v < 0) (see emit_ac): x = the accumulator's start value (2^16, plus kRow0Bias for
+// t = v - (v < 0) (see emit_block): x = the accumulator's start value (2^16, plus kRow0Bias for
 // row 0, columns 1-7), y = qmat, z = the pass-2 row's byte offset in s_m2, w = the column's
 // byte offset in the row image.  One 16-byte LDS read per candidate replaces the zigzag, qmat
 // and row tables and every field extraction.
@@ -331,23 +336,9 @@ __device__ __forceinline__ int exact_coef_t(const uint32_t *pkcol, uint4 d, cons
 // testsrc2 4K q5, so the loop is short.)
 // t: the coefficient v as v - (v < 0) (exact_coef_t), so t is 0 or -1 exactly when v == 0
 // and the category is 32 - v_ffbh_i32(t) (no |v|, no sign fix-up).
-template <class Sink>
-__device__ __forceinline__ void emit_ac(int k, int t, int &prev, Sink &sink) {
-  const int fb = ffbh_i32(t);
-  if (fb < 0) return;  // screened in, quantises to zero
-  int run = k - prev - 1;
-  prev = k;
-  while (run >= 16) {
-    sink.ac(0xf0, 0, 0u);  // ZRL
-    run -= 16;
-  }
-  const int cat = 32 - fb;
-  const uint32_t mant = __builtin_amdgcn_ubfe((uint32_t)t, 0u, (uint32_t)cat);
-  sink.ac(((run & 15) << 4) | cat, cat, mant);
-}
-
-// Candidates are taken two at a time so the LDS reads of both (zigzag -> natural index,
-// the column of the row image, the quantiser) are in flight together.
+// Candidates are taken two at a time so the LDS reads of both (their descriptors, the columns
+// of the row image, then their AC codes) are in flight together: both symbols are formed
+// before either is emitted (the second one's run depends only on whether the first is zero).
 template <class Sink>
 __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand, int diff,
                                            const uint4 *zd, const uint32_t *m2, Sink &sink) {
@@ -365,8 +356,21 @@ __device__ __forceinline__ void emit_block(const uint32_t *pkcol, uint64_t cand,
     cand &= cand - 1;  // no-op when cand == 0
     const int t1 = exact_coef_t(pkcol, zd[k1], m2);
     const int t2 = exact_coef_t(pkcol, zd[k2], m2);
-    emit_ac(k1, t1, prev, sink);
-    if (two) emit_ac(k2, t2, prev, sink);
+    const int fb1 = ffbh_i32(t1), fb2 = two ? ffbh_i32(t2) : -1;  // < 0: quantises to zero
+    const bool nz1 = fb1 >= 0, nz2 = fb2 >= 0;
+    const int run1 = k1 - prev - 1, p1 = nz1 ? k1 : prev, run2 = k2 - p1 - 1;
+    const int cat1 = 32 - fb1, cat2 = 32 - fb2;
+    const int s1 = nz1 ? ((run1 & 15) << 4) | cat1 : 0, s2 = nz2 ? ((run2 & 15) << 4) | cat2 : 0;
+    const uint32_t e1 = sink.lookup(s1), e2 = sink.lookup(s2);
+    if (nz1) {
+      for (int r = run1; r >= 16; r -= 16) sink.ac(0xf0, 0, 0u);  // ZRL
+      sink.put_ac(e1, s1, cat1, __builtin_amdgcn_ubfe((uint32_t)t1, 0u, (uint32_t)cat1));
+    }
+    if (nz2) {
+      for (int r = run2; r >= 16; r -= 16) sink.ac(0xf0, 0, 0u);
+      sink.put_ac(e2, s2, cat2, __builtin_amdgcn_ubfe((uint32_t)t2, 0u, (uint32_t)cat2));
+    }
+    prev = nz2 ? k2 : p1;
   }
   if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB
 }
@@ -499,6 +503,8 @@ struct CountSink {
     rec[n * 64] = ((uint32_t)sym << 16) | mant;
     n++;
   }
+  __device__ __forceinline__ uint32_t lookup(int) const { return 0u; }
+  __device__ __forceinline__ void put_ac(uint32_t, int sym, int cat, uint32_t mant) { ac(sym, cat, mant); }
   __device__ __forceinline__ void finish() {}
 };
 

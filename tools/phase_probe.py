@@ -54,6 +54,25 @@ def main():
               f"({nchunks} chunk-waves)")
         for i, p in enumerate(PHASES):
             print(f"  {p:36s} {acc[i] / nchunks:8.0f}  {100 * acc[i] / max(tot, 1):5.1f}%")
+        # per-wave start / end (s_memrealtime, 100 MHz) of one more launch: the drain at its end
+        L.mjg_probe_waves.argtypes = [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
+        t0, t1 = (C.c_ulonglong * 16384)(), (C.c_ulonglong * 16384)()
+        L.mjg_probe_waves(t0, t1)
+        enc.submit(device_ptr=pool.data_ptr(), nframes=N)
+        enc.sync()
+        L.mjg_probe_waves(t0, t1)
+        import numpy as np
+        a, b = np.array(t0[:]), np.array(t1[:])
+        ok = (a > 0) & (b > 0)
+        a, b = a[ok].astype(np.float64), b[ok].astype(np.float64)
+        span = (b.max() - a.min()) / 100.0  # us
+        busy = (b - a).sum() / 100.0
+        ends = np.sort((b.max() - b) / 100.0)
+        starts = np.sort((a - a.min()) / 100.0)
+        print(f"  waves {ok.sum()}: launch span {span:.1f} us, wave-time utilisation {busy / (ok.sum() * span):.3f}; "
+              f"start spread p50/p99/max {starts[len(starts) // 2]:.1f}/{starts[int(len(starts) * .99)]:.1f}/"
+              f"{starts[-1]:.1f} us; idle before the launch end p10/p50/p90/max "
+              f"{ends[len(ends) // 10]:.1f}/{ends[len(ends) // 2]:.1f}/{ends[int(len(ends) * .9)]:.1f}/{ends[-1]:.1f} us")
         enc.close()
 
 
