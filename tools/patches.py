@@ -86,6 +86,7 @@ PATCHES = {
 _PH_DECL = "constexpr int kWavesPerWg = 4;\n"
 _PH_DEVICE = (_PH_DECL + "__device__ unsigned long long mjg_phase_acc[8];\n"
               "__device__ unsigned long long mjg_wave_t0[16384], mjg_wave_t1[16384];\n"
+              "__device__ unsigned int mjg_wave_hw[16384], mjg_wave_xcc[16384], mjg_wave_n[16384];\n"
               "#define MJG_PH(i) do { if (MODE == kEmitDefault) { __builtin_amdgcn_sched_barrier(0); "
               "const unsigned long long _t = __builtin_amdgcn_s_memtime(); ph_acc[i] += _t - ph_prev; ph_prev = _t; "
               "__builtin_amdgcn_sched_barrier(0); } } while (0)\n")
@@ -97,7 +98,8 @@ def _phase_clock(a):
         (K, "  while (true) {\n    // the next unit is reserved",
          "  unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_prev = __builtin_amdgcn_s_memtime();\n"
          "  if (MODE == kEmitDefault && lane == 0 && gw < 16384) mjg_wave_t0[gw] = __builtin_amdgcn_s_memrealtime();\n"
-         "  while (true) {\n    MJG_PH(7);\n    // the next unit is reserved"),
+         "  unsigned int ph_n = 0;\n"
+         "  while (true) {\n    MJG_PH(7);\n    ph_n++;\n    // the next unit is reserved"),
         (K, "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);\n", "      row_pass<RC>(raw, tab, s_rc, s_pk, lane);\n    MJG_PH(0);\n"),
         (K, "    uint32_t mlo = 0, mhi = 0;  // candidate mask", "    MJG_PH(1);\n    uint32_t mlo = 0, mhi = 0;  // candidate mask"),
         (K, "    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;\n", "    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;\n    MJG_PH(2);\n"),
@@ -108,7 +110,9 @@ def _phase_clock(a):
          "    if (tn < 0) break;"),
         (K, "  if (MODE == kCount && aux_frame >= 0) {\n    asm volatile",
          "  if (MODE == kEmitDefault && lane == 0)\n    for (int i = 0; i < 8; i++) atomicAdd(&mjg_phase_acc[i], ph_acc[i]);\n"
-         "  if (MODE == kEmitDefault && lane == 0 && gw < 16384) mjg_wave_t1[gw] = __builtin_amdgcn_s_memrealtime();\n"
+         "  if (MODE == kEmitDefault && lane == 0 && gw < 16384) {\n    mjg_wave_t1[gw] = __builtin_amdgcn_s_memrealtime();\n"
+         "    mjg_wave_hw[gw] = __builtin_amdgcn_s_getreg((31 << 11) | 4);\n"
+         "    mjg_wave_xcc[gw] = __builtin_amdgcn_s_getreg((31 << 11) | 20);\n    mjg_wave_n[gw] = ph_n;\n  }\n"
          "  if (MODE == kCount && aux_frame >= 0) {\n    asm volatile"),
         ("api.hip", "}  // extern \"C\"", "int mjg_probe_phase(unsigned long long *out) {\n"
          "  HIP_TRY(hipDeviceSynchronize());\n  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(mjg_phase_acc), 64));\n"
@@ -118,6 +122,9 @@ def _phase_clock(a):
          "  HIP_TRY(hipDeviceSynchronize());\n"
          "  HIP_TRY(hipMemcpyFromSymbol(t0, HIP_SYMBOL(mjg_wave_t0), 16384 * 8));\n"
          "  HIP_TRY(hipMemcpyFromSymbol(t1, HIP_SYMBOL(mjg_wave_t1), 16384 * 8));\n"
+         "  HIP_TRY(hipMemcpyFromSymbol(t0 + 16384, HIP_SYMBOL(mjg_wave_hw), 16384 * 4));\n"
+         "  HIP_TRY(hipMemcpyFromSymbol(t0 + 16384 + 8192, HIP_SYMBOL(mjg_wave_xcc), 16384 * 4));\n"
+         "  HIP_TRY(hipMemcpyFromSymbol(t1 + 16384, HIP_SYMBOL(mjg_wave_n), 16384 * 4));\n"
          "  std::vector<unsigned long long> z(16384, 0ull);\n"
          "  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mjg_wave_t0), z.data(), 16384 * 8));\n"
          "  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mjg_wave_t1), z.data(), 16384 * 8));\n"

@@ -56,14 +56,18 @@ def main():
             print(f"  {p:36s} {acc[i] / nchunks:8.0f}  {100 * acc[i] / max(tot, 1):5.1f}%")
         # per-wave start / end (s_memrealtime, 100 MHz) of one more launch: the drain at its end
         L.mjg_probe_waves.argtypes = [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
-        t0, t1 = (C.c_ulonglong * 16384)(), (C.c_ulonglong * 16384)()
+        t0, t1 = (C.c_ulonglong * 32768)(), (C.c_ulonglong * 32768)()  # + hw ids / chunk counts
         L.mjg_probe_waves(t0, t1)
         enc.submit(device_ptr=pool.data_ptr(), nframes=N)
         enc.sync()
         L.mjg_probe_waves(t0, t1)
         import numpy as np
-        a, b = np.array(t0[:]), np.array(t1[:])
+        ext0 = np.frombuffer(bytes(t0), dtype=np.uint32)[32768:]   # hw_id[16384], xcc_id[16384]
+        ext1 = np.frombuffer(bytes(t1), dtype=np.uint32)[32768:]   # chunks per wave
+        hw, xcc, nch = ext0[:16384], ext0[16384:], ext1[:16384]
+        a, b = np.array(t0[:16384]), np.array(t1[:16384])
         ok = (a > 0) & (b > 0)
+        hw, xcc, nch = hw[ok], xcc[ok] & 0xf, nch[ok]
         a, b = a[ok].astype(np.float64), b[ok].astype(np.float64)
         span = (b.max() - a.min()) / 100.0  # us
         busy = (b - a).sum() / 100.0
@@ -73,6 +77,20 @@ def main():
               f"start spread p50/p99/max {starts[len(starts) // 2]:.1f}/{starts[int(len(starts) * .99)]:.1f}/"
               f"{starts[-1]:.1f} us; idle before the launch end p10/p50/p90/max "
               f"{ends[len(ends) // 10]:.1f}/{ends[len(ends) // 2]:.1f}/{ends[int(len(ends) * .9)]:.1f}/{ends[-1]:.1f} us")
+        busyw = (b - a) / 100.0
+        end_idle = (b.max() - b) / 100.0
+        simd = (hw >> 4) & 3
+        cu = (hw >> 8) & 15
+        se = (hw >> 13) & 3
+        for name, key in (("xcc", xcc), ("simd", simd), ("se", se)):
+            parts = [f"{int(v)}: busy {busyw[key == v].mean():.0f} us, chunks {nch[key == v].mean():.1f}, "
+                     f"us/chunk {(busyw[key == v] / np.maximum(nch[key == v], 1)).mean():.2f}, end-idle "
+                     f"{end_idle[key == v].mean():.0f}" for v in np.unique(key)]
+            print(f"  by {name}: " + " | ".join(parts))
+        slot = hw & 15  # wave slot on its SIMD
+        parts = [f"{int(v)}: us/chunk {(busyw[slot == v] / np.maximum(nch[slot == v], 1)).mean():.2f} "
+                 f"chunks {nch[slot == v].mean():.1f}" for v in np.unique(slot)]
+        print("  by wave slot: " + " | ".join(parts))
         enc.close()
 
 
