@@ -135,6 +135,27 @@ def _phase_clock(a):
 PATCHES["phase_clock"] = _phase_clock
 
 
+# ---------------------------------------------------------------- wave priority experiments (r04)
+# The SIMD arbiter favours its oldest wave: per chunk, wave slot 0 runs 2.2x faster than slot 3
+# (profiles/r04j_drain_by_hw.txt), so at the end of a launch the slowest waves hold the last units.
+_NEXT = "      tn = nbu < nbatch ? nbu * kBatch : -1;\n"
+PATCHES["prio_late"] = lambda a: [(K, _NEXT, _NEXT +
+    "      if (nbu < nbatch) {  // a unit among the last of its eighth: run it at top priority\n"
+    "        const int xe = (int)(((long long)nbu * NX) / nbatch);\n"
+    "        int e = xu.start(xe + 1);\n"
+    "        if (nbu >= e) e = xu.start(xe + 2);\n"
+    "        if (e - nbu <= " + str(int(a or 512)) + ") __builtin_amdgcn_s_setprio(3);\n"
+    "      }\n")]
+PATCHES["prio_slot"] = lambda a: [(K, "  __syncthreads();  // tables visible; the only workgroup barrier\n",
+    "  __syncthreads();  // tables visible; the only workgroup barrier\n"
+    "  {  // equalise the arbiter: younger wave slots get higher priority\n"
+    "    const uint32_t slot = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg((3 << 11) | 4)) & 3u;\n"
+    "    if (slot == 1) __builtin_amdgcn_s_setprio(1);\n"
+    "    if (slot == 2) __builtin_amdgcn_s_setprio(2);\n"
+    "    if (slot == 3) __builtin_amdgcn_s_setprio(3);\n"
+    "  }\n")]
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
