@@ -317,10 +317,11 @@ def roofline_entry(kernel, alg_bytes, ms, traffic, what):
 
 def rooflines(kt, seg, mean_jpeg, pmc, optimal, scaled, step_ms=None):
     """Per-kernel roofline entries (SURVEY §8d bytes) and the primary one (reads the input).
-    step_ms: with -huffman optimal or -vf scale the submits of consecutive segments run on two
-    streams and their launches overlap (csrc/api.hip alloc_slot), so a kernel's event interval
-    includes time shared with the other submit's kernels; the primary entry is then the whole
-    chain's bytes over the wall time per step (the per-kernel entries stay as measured)."""
+    step_ms: the submits of consecutive segments run on two streams and their launches overlap
+    (csrc/api.hip alloc_slot: the next launch starts in the previous one's drain), so a kernel's
+    event interval includes time shared with the other submit's kernels; the primary entry is
+    then the bytes of one step over the wall time per step (the per-kernel entries stay as
+    measured, overlap included)."""
     src_b, dst_b, jpeg_b = frame_bytes(W, H) * seg, frame_bytes(DW, DH) * seg, mean_jpeg * seg
     out = []
     if scaled and kt.get("scale", 0) > 0:  # unfused: k_scale writes the scaled planes to HBM
@@ -350,6 +351,9 @@ def rooflines(kt, seg, mean_jpeg, pmc, optimal, scaled, step_ms=None):
         if scaled and step_ms:
             primary = roofline_entry("k_scale + k_encode, wall time per step", src_b + jpeg_b, step_ms,
                                      None, "source planes read + JPEG written")
+        elif step_ms:
+            primary = roofline_entry(name + ", wall time per step (launches overlap)", enc_in + jpeg_b, step_ms,
+                                     out[0]["traffic"], out[0]["bytes"])
     return primary, out
 
 
@@ -444,7 +448,7 @@ def main():
     pmc, pmc_src = (load_pmc(a.workload, a.content, B.source_digest())
                     if (seg == SEG and not a.rst and not a.fused and a.dct == "auto"
                         and HUFF == WORKLOADS[a.workload][7]) else ({}, "no PMC pass for this configuration"))
-    overlap = HUFF == "optimal" or (DW, DH) != (W, H)  # two submit streams (see rooflines)
+    overlap = True  # consecutive submits run on two streams (csrc/api.hip alloc_slot; see rooflines)
     primary, per_kernel = rooflines(kt, seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H),
                                     dt / a.steps * 1e3 if overlap else None)
     primary = dict(primary, launches=nl, traffic_source=pmc_src)

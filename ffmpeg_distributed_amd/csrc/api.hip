@@ -404,13 +404,13 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   const size_t B = c->slot_B, NC = c->slot_NC, NS = c->slot_NS;
   const EncGeom &g = c->geom;
   int rc;
-  // Slot 1 on its own stream where a submit is a chain of launches that each drain the GPU
-  // (-huffman optimal: count pass, table build, emission; -vf scale: k_scale, k_encode): the
-  // next submit's chain then starts on the CUs the previous one's drains free (A/B: c1 +24%,
-  // c4 +1.7%).  A plain default-table submit is one k_encode launch: overlapping consecutive
-  // launches measured +1.1% (c2) while each launch's own time grew 5%, so those stay on one
-  // stream (launches back to back, per-launch times comparable).
-  S.st = (&S == &c->slot[1] && (c->optimal || c->scale)) ? c->stream2 : c->stream;
+  // Slot 1 on its own stream: consecutive submits (queued two deep) overlap, so the next
+  // submit's launches start on the CUs the previous one's drain frees.  A persistent k_encode's
+  // waves finish its last work units over ~140 us (the SIMD arbiter runs its oldest wave 2.2x
+  // faster than its youngest), and a workgroup's slot frees when its last wave
+  // ends.  A/B: c2 +5.4% (bench.py, r04), c5 +1.6%, c1 +24% and c4 +1.7% (r03, chains of
+  // launches).  Each launch's own event interval then includes its neighbour's overlap.
+  S.st = &S == &c->slot[1] ? c->stream2 : c->stream;
   if ((rc = dmalloc(&S.d_stage_bits, c->stage_cols * 64 * kStageWords))) return rc;
   if (c->scale && !c->fused && (rc = dmalloc(&S.d_scaled, B * c->enc_frame_bytes))) return rc;
   if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||

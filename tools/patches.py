@@ -155,6 +155,11 @@ PATCHES["prio_slot"] = lambda a: [(K, "  __syncthreads();  // tables visible; th
     "    if (slot == 3) __builtin_amdgcn_s_setprio(3);\n"
     "  }\n")]
 
+# default-table submits back to back on one stream (round 3's form; two streams since r04,
+# profiles/r04m_ab_two_streams_bench.txt)
+PATCHES["one_stream"] = lambda a: [("api.hip", "  S.st = &S == &c->slot[1] ? c->stream2 : c->stream;",
+                                    "  S.st = (&S == &c->slot[1] && (c->optimal || c->scale)) ? c->stream2 : c->stream;")]
+
 
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
