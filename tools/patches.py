@@ -160,6 +160,13 @@ PATCHES["prio_slot"] = lambda a: [(K, "  __syncthreads();  // tables visible; th
 PATCHES["one_stream"] = lambda a: [("api.hip", "  S.st = &S == &c->slot[1] ? c->stream2 : c->stream;",
                                     "  S.st = (&S == &c->slot[1] && (c->optimal || c->scale)) ? c->stream2 : c->stream;")]
 
+# probes (wrong output): the stuffing tail's co-run cost on the bench (the kernels launch, and
+# return at once)
+PATCHES["no_write"] = lambda a: [(K, "  const int gi = blockIdx.x * 4 + wave, ngroups = gps * nseg * nframes;\n  if (gi >= ngroups) return;",
+                                  "  const int gi = blockIdx.x * 4 + wave, ngroups = gps * nseg * nframes;\n  if (gi >= 0) return;")]
+PATCHES["no_count"] = lambda a: [(K, "  for (int i = lane; i < 64 * kTailRounds; i += 64) s_marks[wave][i] = 0;\n  if (gi >= ngroups) return;",
+                                  "  for (int i = lane; i < 64 * kTailRounds; i += 64) s_marks[wave][i] = 0;\n  if (gi >= 0) return;")]
+
 
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
