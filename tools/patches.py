@@ -168,6 +168,100 @@ PATCHES["no_count"] = lambda a: [(K, "  for (int i = lane; i < 64 * kTailRounds;
                                   "  for (int i = lane; i < 64 * kTailRounds; i += 64) s_marks[wave][i] = 0;\n  if (gi >= 0) return;")]
 
 
+# emit_block taking four candidates per step instead of two (more LDS reads in flight)
+_PAIR_OLD = """  while (cand) {
+    const int k1 = (int)__builtin_ctzll(cand);"""
+_PAIR_END = """    prev = nz2 ? k2 : p1;
+  }
+"""
+_QUAD = """  while (cand) {
+    int kq[4], tq[4], fq[4];
+    bool hq[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      hq[i] = cand != 0;
+      kq[i] = hq[i] ? (int)__builtin_ctzll(cand) : 0;
+      cand &= cand - 1;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) tq[i] = exact_coef_t(pkcol, zd[kq[i]], m2);
+    int p = prev, sq[4], rq[4];
+    uint32_t eq[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      fq[i] = hq[i] ? ffbh_i32(tq[i]) : -1;
+      rq[i] = kq[i] - p - 1;
+      p = fq[i] >= 0 ? kq[i] : p;
+      sq[i] = fq[i] >= 0 ? ((rq[i] & 15) << 4) | (32 - fq[i]) : 0;
+      eq[i] = sink.lookup(sq[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (fq[i] >= 0) {
+        for (int r = rq[i]; r >= 16; r -= 16) sink.ac(0xf0, 0, 0u);
+        sink.put_ac(eq[i], sq[i], 32 - fq[i], __builtin_amdgcn_ubfe((uint32_t)tq[i], 0u, (uint32_t)(32 - fq[i])));
+      }
+    prev = p;
+  }
+"""
+
+
+def _quad(a):
+    src = open(os.path.join(CSRC, K)).read()
+    i = src.index(_PAIR_OLD)
+    j = src.index(_PAIR_END, i) + len(_PAIR_END)
+    return [(K, src[i:j], _QUAD)]
+
+
+PATCHES["quad"] = _quad
+
+
+# the chunk-parallel coder prototype (tools/cpc_proto.hip) in place of the per-lane emission,
+# the wave-parallel blocks and pack_chunk
+_CPC_OLD_START = "    const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);\n"
+_CPC_OLD_END = "    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n"
+
+
+def _cpc(a):
+    src = open(os.path.join(CSRC, K)).read()
+    i = src.index(_CPC_OLD_START)
+    j = src.index(_CPC_OLD_END, i) + len(_CPC_OLD_END)
+    proto = open(os.path.join(HERE, "cpc_proto.hip")).read()
+    hv = "  uint32_t *s_hv = s_hv_all[MODE == kEmitDefault ? wave : 0];\n"
+    return [
+        (K, "template <int NX>\nstruct XcdUnits {", proto + "template <int NX>\nstruct XcdUnits {"),
+        (K, hv, hv + "  __shared__ uint32_t s_ring_all[MODE == kEmitDefault ? kWavesPerWg : 1][kRingWords];\n"
+                     "  if (MODE == kEmitDefault)\n"
+                     "    for (int i = lane; i < kRingWords; i += 64) s_ring_all[wave][i] = 0u;\n"),
+        (K, src[i:j], "    emit_chunk_cpc(s_pk, lane, cur_active, mask, diff, tab, s_zd, s_m2, s_ac, s_dc,\n"
+                      "                   s_ring_all[MODE == kEmitDefault ? wave : 0], stage_w,\n"
+                      "                   scratch + (size_t)t * kSlotWords, chunk_bits + t);\n"),
+    ]
+
+
+PATCHES["cpc"] = _cpc
+
+
+def _cpc_hybrid(a):
+    """the prototype only for chunks whose per-lane cost exceeds a * rounds"""
+    src = open(os.path.join(CSRC, K)).read()
+    i = src.index(_CPC_OLD_START)
+    j = src.index(_CPC_OLD_END, i) + len(_CPC_OLD_END)
+    p = _cpc(a)
+    p[2] = (K, src[i:j],
+            "    const int nc_h = cur_active ? __popcll(mask) : 0;\n"
+            "    const int rounds_h = (wave_sum(cur_active ? nc_h + 1 : 0) + 63) >> 6;\n"
+            f"    if (per_lane_cost(nc_h) > {float(a)}f * rounds_h) {{\n"
+            "    emit_chunk_cpc(s_pk, lane, cur_active, mask, diff, tab, s_zd, s_m2, s_ac, s_dc,\n"
+            "                   s_ring_all[MODE == kEmitDefault ? wave : 0], stage_w,\n"
+            "                   scratch + (size_t)t * kSlotWords, chunk_bits + t);\n"
+            "    } else {\n" + src[i:j] + "    }\n")
+    return p
+
+
+PATCHES["cpc_hybrid"] = _cpc_hybrid
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
