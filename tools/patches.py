@@ -262,6 +262,26 @@ def _cpc_hybrid(a):
 PATCHES["cpc_hybrid"] = _cpc_hybrid
 
 
+# HIP stream priorities: the stuffing tail's stream at the lowest priority ("tail"), or also
+# both submit streams at the highest ("both"), so k_encode's workgroups dispatch first
+_STREAMS = ("  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));\n"
+            "  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));\n"
+            "  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));\n")
+
+
+def _stream_prio(a):
+    hi = "greatest" if a == "both" else "0"
+    return [("api.hip", _STREAMS,
+             "  int least = 0, greatest = 0;\n"
+             "  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));\n"
+             f"  HIP_TRY(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, {hi}));\n"
+             f"  HIP_TRY(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, {hi}));\n"
+             "  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, least));\n")]
+
+
+PATCHES["stream_prio"] = _stream_prio
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
