@@ -279,6 +279,7 @@ struct ShiftSink {
 };
 
 constexpr int kStageWords = (kMaxBlockBits + 31) / 32;  // staged words per lane
+constexpr int kHvWords = kStageWords < 64 ? 64 : kStageWords;  // s_hv: emit_block_wave, pack_chunk_short
 
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
 // image (pkcol = s_pk + lane: word [c*4 + r/2] holds column c of rows r, r+1 (r even) as u16
@@ -742,6 +743,26 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
   if (lane == 0) *chunk_bits_t = total;
 }
 
+// pack_chunk for a chunk whose blocks are all at most 32 bits (window path only; 96% of
+// testsrc 4K q5 chunks): each block's bits, right-aligned in w3, are ORed into the wave's LDS
+// words (s_w, zero outside a pack, >= 64 words: a chunk is then at most 2048 bits), which one
+// coalesced store moves to the slot.  No per-word opener logic; same bytes as pack_chunk.
+__device__ __forceinline__ void pack_chunk_short(const ShiftSink &q, uint32_t bits, uint32_t *s_w, uint32_t *slot,
+                                                 uint32_t *chunk_bits_t, int lane) {
+  const uint32_t incl = wave_incl_scan(bits, lane), off = incl - bits, total = lane63(incl);
+  if (bits) {  // bits [off, off + bits), MSB first: at most two words
+    const uint64_t x = (uint64_t)q.w3 << (64u - (off & 31u) - bits);
+    atomicOr(s_w + (off >> 5), (uint32_t)(x >> 32));
+    if ((uint32_t)x) atomicOr(s_w + (off >> 5) + 1, (uint32_t)x);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((uint32_t)lane < ((total + 31u) >> 5)) {
+    slot[lane] = s_w[lane];
+    s_w[lane] = 0u;
+  }
+  if (lane == 0) *chunk_bits_t = total;
+}
+
 // Row pass of one chunk, lane = block: raw rows (8 little-endian words of 8 pixels) ->
 // the wave's LDS row image s_pk ([word][lane]; word c*4 + r/2 = column c of rows r, r+1 as
 // u16 pairs; output 0 as is, 1-7 + 16384).
@@ -1143,7 +1164,8 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint4 s_bd[16];                       // their plane fields (BlockDesc)
   __shared__ uint32_t s_skip[SCR ? 12 : 1];        // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
-  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kStageWords];  // emit_block_wave
+  // emit_block_wave's stream words, pack_chunk_short's chunk words
+  __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kHvWords];
   // per wave: the current frame's histogram (kCount)
   __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][MODE == kEmitDefault ? 1 : kFrameTabWords];
 
@@ -1171,7 +1193,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   uint32_t *s_pk = s_pk_all[wave];
   uint32_t *s_hv = s_hv_all[MODE == kEmitDefault ? wave : 0];
   if (MODE == kEmitDefault)
-    for (int i = lane; i < kStageWords; i += 64) s_hv[i] = 0u;
+    for (int i = lane; i < kHvWords; i += 64) s_hv[i] = 0u;
   uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
   if (MODE == kCount)
     for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
@@ -1311,7 +1333,11 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged words visible to pack_chunk's lanes
     }
-    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+    const uint32_t qbits = cur_active ? q.bits : 0u;
+    if (__ballot(qbits > 32u || q.staged) == 0ull)
+      pack_chunk_short(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+    else
+      pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     if (tn < 0) break;
     if (new_batch) {
       carry = carry_finish(crow, chunk, lane, rc, g, s_desc);

@@ -74,7 +74,7 @@ PATCHES = {
     B[i] = nB ? B[i] : 0u;
 """)],
     # occupancy probe: k_encode's workgroup LDS past 40 KB (3 workgroups, 3 waves per SIMD)
-    "occ3": lambda a: [(K, "][kStageWords];  // emit_block_wave", "][kStageWords + 512];  // emit_block_wave")],
+    "occ3": lambda a: [(K, "][kHvWords];\n", "][kHvWords + 512];\n")],
 }
 
 # ---------------------------------------------------------------- probes (wrong timing, right bytes)
@@ -105,8 +105,9 @@ def _phase_clock(a):
         (K, "    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;\n", "    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;\n    MJG_PH(2);\n"),
         (K, "    if (cur_active && !((wide >> lane) & 1ull)) {", "    MJG_PH(3);\n    if (cur_active && !((wide >> lane) & 1ull)) {"),
         (K, "    if (wide) {  // the heavy blocks", "    MJG_PH(4);\n    if (wide) {  // the heavy blocks"),
-        (K, "    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    if (tn < 0) break;",
-         "    MJG_PH(5);\n    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    MJG_PH(6);\n"
+        (K, "    const uint32_t qbits = cur_active ? q.bits : 0u;\n", "    MJG_PH(5);\n    const uint32_t qbits = cur_active ? q.bits : 0u;\n"),
+        (K, "      pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    if (tn < 0) break;",
+         "      pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n    MJG_PH(6);\n"
          "    if (tn < 0) break;"),
         (K, "  if (MODE == kCount && aux_frame >= 0) {\n    asm volatile",
          "  if (MODE == kEmitDefault && lane == 0)\n    for (int i = 0; i < 8; i++) atomicAdd(&mjg_phase_acc[i], ph_acc[i]);\n"
@@ -219,7 +220,7 @@ PATCHES["quad"] = _quad
 # the chunk-parallel coder prototype (tools/cpc_proto.hip) in place of the per-lane emission,
 # the wave-parallel blocks and pack_chunk
 _CPC_OLD_START = "    const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);\n"
-_CPC_OLD_END = "    pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n"
+_CPC_OLD_END = "      pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);\n"
 
 
 def _cpc(a):
@@ -280,6 +281,15 @@ def _stream_prio(a):
 
 
 PATCHES["stream_prio"] = _stream_prio
+
+
+# pack_chunk for every chunk, without pack_chunk_short's fast path for chunks of short blocks
+# (profiles/r04t_ab_short_pack.txt; that record also holds a measured-and-not-kept variant for
+# blocks up to 64 bits and chunks up to 64 words)
+PATCHES["no_short_pack"] = lambda a: [(K, """    if (__ballot(qbits > 32u || q.staged) == 0ull)
+      pack_chunk_short(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+    else
+""", "")]
 
 
 def parse_spec(spec: str):
