@@ -279,7 +279,7 @@ struct ShiftSink {
 };
 
 constexpr int kStageWords = (kMaxBlockBits + 31) / 32;  // staged words per lane
-constexpr int kHvWords = kStageWords < 64 ? 64 : kStageWords;  // s_hv: emit_block_wave, pack_chunk_short
+constexpr int kHvWords = kStageWords < 128 ? 128 : kStageWords;  // s_hv: emit_block_wave, pack_chunk_short
 
 // Exact quantised coefficient at natural index n of this lane's block, from the row-pass
 // image (pkcol = s_pk + lane: word [c*4 + r/2] holds column c of rows r, r+1 (r even) as u16
@@ -743,23 +743,40 @@ __device__ __forceinline__ void pack_chunk(const ShiftSink &q, bool cur_active, 
   if (lane == 0) *chunk_bits_t = total;
 }
 
-// pack_chunk for a chunk whose blocks are all at most 32 bits (window path only; 96% of
-// testsrc 4K q5 chunks): each block's bits, right-aligned in w3, are ORed into the wave's LDS
-// words (s_w, zero outside a pack, >= 64 words: a chunk is then at most 2048 bits), which one
-// coalesced store moves to the slot.  No per-word opener logic; same bytes as pack_chunk.
+// pack_chunk for a chunk whose blocks are all short and none wave-parallel (window path only):
+// each block's bits, right-aligned in the queue, are ORed into the wave's LDS words (s_w, zero
+// outside a pack, >= 128 words), which coalesced stores move to the slot.  No per-word opener
+// logic; same bytes as pack_chunk.  W = 32: blocks of at most 32 bits (w3; two words at most;
+// 96% of testsrc 4K q5 chunks), W = 64: at most 64 bits (w2:w3; three words; 2/3 of the
+// fractal content's chunks).  A chunk is then at most 64 x W bits.
+template <int W>
 __device__ __forceinline__ void pack_chunk_short(const ShiftSink &q, uint32_t bits, uint32_t *s_w, uint32_t *slot,
                                                  uint32_t *chunk_bits_t, int lane) {
   const uint32_t incl = wave_incl_scan(bits, lane), off = incl - bits, total = lane63(incl);
-  if (bits) {  // bits [off, off + bits), MSB first: at most two words
-    const uint64_t x = (uint64_t)q.w3 << (64u - (off & 31u) - bits);
-    atomicOr(s_w + (off >> 5), (uint32_t)(x >> 32));
-    if ((uint32_t)x) atomicOr(s_w + (off >> 5) + 1, (uint32_t)x);
+  if (bits) {  // bits [off, off + bits), MSB first
+    uint32_t *d = s_w + (off >> 5);
+    if (W == 32) {
+      const uint64_t x = (uint64_t)q.w3 << (64u - (off & 31u) - bits);
+      atomicOr(d, (uint32_t)(x >> 32));
+      if ((uint32_t)x) atomicOr(d + 1, (uint32_t)x);
+    } else {  // emit_block_wave's placement: V << sh fits 96 bits
+      const uint64_t v = ((uint64_t)q.w2 << 32) | q.w3;
+      const uint32_t sh = 96u - (off & 31u) - bits;
+      const uint64_t hi = sh >= 32u ? v << (sh - 32u) : v >> (32u - sh);
+      const uint32_t lo = sh >= 32u ? 0u : (uint32_t)(v << sh);
+      atomicOr(d, (uint32_t)(hi >> 32));
+      if ((uint32_t)hi) atomicOr(d + 1, (uint32_t)hi);
+      if (lo) atomicOr(d + 2, lo);
+    }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if ((uint32_t)lane < ((total + 31u) >> 5)) {
-    slot[lane] = s_w[lane];
-    s_w[lane] = 0u;
-  }
+  const uint32_t nw = (total + 31u) >> 5;
+#pragma unroll
+  for (uint32_t w = (uint32_t)lane; w < (uint32_t)(2 * W); w += 64)
+    if (w < nw) {
+      slot[w] = s_w[w];
+      s_w[w] = 0u;
+    }
   if (lane == 0) *chunk_bits_t = total;
 }
 
@@ -1335,7 +1352,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     }
     const uint32_t qbits = cur_active ? q.bits : 0u;
     if (__ballot(qbits > 32u || q.staged) == 0ull)
-      pack_chunk_short(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+      pack_chunk_short<32>(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+    else if (__ballot(qbits > 64u || q.staged) == 0ull)
+      pack_chunk_short<64>(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     else
       pack_chunk(q, cur_active, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     if (tn < 0) break;

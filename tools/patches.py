@@ -284,12 +284,19 @@ PATCHES["stream_prio"] = _stream_prio
 
 
 # pack_chunk for every chunk, without pack_chunk_short's fast path for chunks of short blocks
-# (profiles/r04t_ab_short_pack.txt; that record also holds a measured-and-not-kept variant for
-# blocks up to 64 bits and chunks up to 64 words)
+# (profiles/r04t_ab_short_pack.txt, r04w_bench_ab_short_pack_pack64.txt)
 PATCHES["no_short_pack"] = lambda a: [(K, """    if (__ballot(qbits > 32u || q.staged) == 0ull)
-      pack_chunk_short(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+      pack_chunk_short<32>(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+    else if (__ballot(qbits > 64u || q.staged) == 0ull)
+      pack_chunk_short<64>(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
     else
 """, "")]
+# only the 32-bit fast path (HEAD 2ffb3a0; profiles/r04w_bench_ab_short_pack_pack64.txt)
+PATCHES["no_pack64"] = lambda a: [(K, """    else if (__ballot(qbits > 64u || q.staged) == 0ull)
+      pack_chunk_short<64>(q, qbits, s_hv, scratch + (size_t)t * kSlotWords, chunk_bits + t, lane);
+""", "")]
+
+
 
 
 def parse_spec(spec: str):
