@@ -264,7 +264,8 @@ PATCHES["cpc_hybrid"] = _cpc_hybrid
 
 
 # HIP stream priorities: the stuffing tail's stream at the lowest priority ("tail"), or also
-# both submit streams at the highest ("both"), so k_encode's workgroups dispatch first
+# both submit streams at the highest ("both"), so k_encode's workgroups dispatch first; or the
+# tail's stream at the highest ("tailhigh"), so a submit's slot is released sooner
 _STREAMS = ("  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));\n"
             "  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));\n"
             "  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));\n")
@@ -272,12 +273,13 @@ _STREAMS = ("  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking
 
 def _stream_prio(a):
     hi = "greatest" if a == "both" else "0"
+    tail = "greatest" if a == "tailhigh" else "least"
     return [("api.hip", _STREAMS,
              "  int least = 0, greatest = 0;\n"
              "  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));\n"
              f"  HIP_TRY(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, {hi}));\n"
              f"  HIP_TRY(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, {hi}));\n"
-             "  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, least));\n")]
+             f"  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, {tail}));\n")]
 
 
 PATCHES["stream_prio"] = _stream_prio
@@ -297,6 +299,21 @@ PATCHES["no_pack64"] = lambda a: [(K, """    else if (__ballot(qbits > 64u || q.
 """, "")]
 
 
+
+
+# the screen's candidate-bit deposit as two forced VALU per coefficient (v_lshrrev of the sign,
+# v_lshl_or into the mask) instead of the compiler's shift / and / or3 form
+_DEPOSIT = """          if (z < 32)
+            mlo |= (neg >> 31) << z;
+          else
+            mhi |= (neg >> 31) << (z - 32);
+"""
+PATCHES["deposit_asm"] = lambda a: [(K, _DEPOSIT, """          const uint32_t sb = neg >> 31;
+          if (z < 32)
+            asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(mlo) : "v"(sb), "n"(z));
+          else
+            asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(mhi) : "v"(sb), "n"(z - 32));
+""")]
 
 
 def parse_spec(spec: str):
