@@ -415,13 +415,15 @@ def main():
                        dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
     bytes_out = []
 
-    # Segments are pipelined two deep (mjg_submit queues up to two): segment s+1's kernels
-    # are queued behind segment s's before s is synced, so the GPU does not idle while the
-    # host collects a segment's sizes and issues the next launches.
+    # Segments are pipelined enc.depth (3) deep, as mjg_submit queues them: later segments'
+    # kernels are queued behind segment s's before s is synced, so the GPU does not idle while
+    # the host collects a segment's sizes and issues the next launches.
+    depth = enc.depth
+
     def step(s):
         base = pool[(s % nseg_pool) * seg]
         enc.submit(device_ptr=base.data_ptr(), nframes=seg)
-        if enc.pending == 2:
+        if enc.pending == depth:
             bytes_out.append(int(enc.sync().sum()))
 
     def drain_and_sync():

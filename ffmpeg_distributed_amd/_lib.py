@@ -41,7 +41,7 @@ MJG_NUM_KERNELS = len(KERNEL_NAMES)
 EXPORTS = (
     "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_device_numa_node", "mjg_open", "mjg_close",
     "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch", "mjg_fetch_host",
-    "mjg_output_device", "mjg_stream", "mjg_host_alloc", "mjg_host_free",
+    "mjg_output_device", "mjg_stream", "mjg_queue_depth", "mjg_host_alloc", "mjg_host_free",
     "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
     "mjg_debug_planes", "mjg_debug_filter",
 )
@@ -96,6 +96,8 @@ def load():
         L.mjg_output_device.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
         L.mjg_stream.argtypes = [vp]
         L.mjg_stream.restype = vp
+        L.mjg_queue_depth.argtypes = []
+        L.mjg_queue_depth.restype = C.c_int
         L.mjg_host_alloc.argtypes = [sz, C.POINTER(vp)]
         L.mjg_host_free.argtypes = [vp]
         L.mjg_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_int]

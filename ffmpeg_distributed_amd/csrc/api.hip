@@ -164,13 +164,19 @@ struct PlaneScale {
   bool fusable = false;  // taps fit the fused kernel (HT 4/8, D4, windows inside the rows)
 };
 
-// Per-submit state.  A context has two slots so a second mjg_submit can be queued before
+// Per-submit state.  A context has kSlots slots so further mjg_submits can be queued before
 // the first is synced; everything a submit's results and its overflow re-write need lives
-// in its slot.  Slot 1 is allocated on the first pipelined submit.  Two streams: the ctx
-// stream runs H2D, scale and k_encode; the tail stream runs a submit's scan/stuff/write
+// in its slot.  Slots 1.. are allocated on the first pipelined submits.  Each slot has its
+// own stream for H2D, scale and k_encode; the tail stream runs a submit's scan/stuff/write
 // kernels after its k_encode (event enc_done), so the latency-bound tail of submit A runs
 // beside the VALU-bound k_encode of submit B.  A slot is reused only after the host synced
 // its previous submit (mjg_sync waits for `done`), so no device-side wait guards it.
+// Two deep: a persistent k_encode holds every CU until its drain, so the host's sync of
+// submit s-1 (whose slot submit s+1 reuses) waits for its tail, which gets CUs only as submit
+// s's k_encode drains; the tail stream therefore runs at the highest priority (its
+// workgroups dispatch before the next k_encode's).  Three slots measured 10% slower: three
+// k_encode launches then share the CUs (DESIGN §4 streams; tools/patches.py slots3).
+constexpr int kSlots = 2;
 struct Slot {
   bool alloc = false, pending = false;
   hipStream_t st = nullptr;        // H2D, scale and k_encode of this slot's submits
@@ -206,8 +212,8 @@ struct mjg_ctx {
   int device = 0;
   mjg_config cfg{};
   hipStream_t stream = nullptr;  // H2D, scale, k_encode of slot 0's submits
-  hipStream_t stream2 = nullptr; // ... of slot 1's: consecutive submits' k_encode launches overlap
-                                 // (the next one starts on the CUs the previous one's drain frees)
+  hipStream_t more[kSlots - 1] = {};  // ... of slots 1..: consecutive submits' k_encode launches
+                                      // overlap (the next starts on the CUs the previous drain frees)
   hipStream_t tail = nullptr;    // scans, stuffing, write, D2H of the sizes
   EncGeom geom{};
   int32_t qmat[64];
@@ -231,9 +237,9 @@ struct mjg_ctx {
   int fused_grid = 0;   // persistent k_scale_encode workgroups
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
 
-  Slot slot[2];
+  Slot slot[kSlots];
   int head = 0;   // slot of the next submit
-  int nout = 0;   // submits queued and not synced (0..2)
+  int nout = 0;   // submits queued and not synced (0..kSlots)
   int last = -1;  // slot of the last synced submit (fetch / output_device / debug read it)
   bool synced_since_submit = false;
 
@@ -250,7 +256,8 @@ void free_ctx(mjg_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  for (hipStream_t st : c->more)
+    if (st) (void)hipStreamSynchronize(st);
   if (c->tail) (void)hipStreamSynchronize(c->tail);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
@@ -275,7 +282,8 @@ void free_ctx(mjg_ctx *c) {
   }
   if (c->h_fetch) (void)hipHostFree(c->h_fetch);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  for (hipStream_t st : c->more)
+    if (st) (void)hipStreamDestroy(st);
   if (c->tail && c->tail != c->stream) (void)hipStreamDestroy(c->tail);
   delete c;
 }
@@ -400,17 +408,19 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   return MJG_OK;
 }
 
+hipStream_t slot_stream(const mjg_ctx *c, int i) { return i ? c->more[i - 1] : c->stream; }
+
 int alloc_slot(mjg_ctx *c, Slot &S) {
   const size_t B = c->slot_B, NC = c->slot_NC, NS = c->slot_NS;
   const EncGeom &g = c->geom;
   int rc;
-  // Slot 1 on its own stream: consecutive submits (queued two deep) overlap, so the next
+  // Each slot on its own stream: consecutive submits (queued kSlots deep) overlap, so the next
   // submit's launches start on the CUs the previous one's drain frees.  A persistent k_encode's
   // waves finish its last work units over ~140 us (the SIMD arbiter runs its oldest wave 2.2x
   // faster than its youngest), and a workgroup's slot frees when its last wave
   // ends.  A/B: c2 +5.4% (bench.py, r04), c5 +1.6%, c1 +24% and c4 +1.7% (r03, chains of
   // launches).  Each launch's own event interval then includes its neighbour's overlap.
-  S.st = &S == &c->slot[1] ? c->stream2 : c->stream;
+  S.st = slot_stream(c, (int)(&S - c->slot));
   if ((rc = dmalloc(&S.d_stage_bits, c->stage_cols * 64 * kStageWords))) return rc;
   if (c->scale && !c->fused && (rc = dmalloc(&S.d_scaled, B * c->enc_frame_bytes))) return rc;
   if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||
@@ -558,8 +568,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   if (device < 0 || device >= ndev) return set_err(MJG_E_INVALID, "device %d of %d", device, ndev);
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));
+  for (hipStream_t &st : c->more) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  int least = 0, greatest = 0;  // the tail's workgroups first (see kSlots)
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, greatest));
 
   c->scale = (k.src_w != k.dst_w || k.src_h != k.dst_h);
   const int cf = k.chroma_format;
@@ -938,11 +950,11 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (!c || !frames) return set_err(MJG_E_INVALID, "null argument");
   if (n < 1 || n > c->cfg.max_batch)
     return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
-  if (c->nout == 2) return set_err(MJG_E_STATE, "two submits queued: sync one first");
+  if (c->nout == kSlots) return set_err(MJG_E_STATE, "%d submits queued: sync one first", kSlots);
   HIP_TRY(hipSetDevice(c->device));
   const EncGeom &g = c->geom;
   Slot &S = c->slot[c->head];
-  if (!S.alloc) {  // the second slot, on the first pipelined submit
+  if (!S.alloc) {  // slots 1.., on the first pipelined submits
     const int rc = alloc_slot(c, S);
     if (rc) return rc;
   }
@@ -1071,7 +1083,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (rc) return rc;
   S.n = n;
   S.pending = true;
-  c->head ^= 1;
+  c->head = (c->head + 1) % kSlots;
   c->nout++;
   c->synced_since_submit = false;
   return MJG_OK;
@@ -1083,7 +1095,7 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
   if (c->nout == 0 && c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
   HIP_TRY(hipSetDevice(c->device));
   if (c->nout > 0) {
-    const int si = c->nout == 2 ? c->head : c->head ^ 1;  // oldest queued submit
+    const int si = (c->head + kSlots - c->nout) % kSlots;  // oldest queued submit
     Slot &S = c->slot[si];
     HIP_TRY(hipEventSynchronize(S.done));
     const int n = S.n;
@@ -1180,7 +1192,12 @@ int mjg_output_device(mjg_ctx *c, const uint8_t **data, const uint64_t **offsets
   return MJG_OK;
 }
 
-void *mjg_stream(mjg_ctx *c) { return c ? (void *)(c->slot[c->head].st ? c->slot[c->head].st : c->stream) : nullptr; }
+void *mjg_stream(mjg_ctx *c) {
+  if (!c) return nullptr;
+  return (void *)slot_stream(c, c->head);
+}
+
+int mjg_queue_depth(void) { return kSlots; }
 
 int mjg_host_alloc(size_t bytes, void **ptr) {
   if (!ptr) return set_err(MJG_E_INVALID, "null argument");

@@ -138,13 +138,18 @@ class MjpegEncoder:
     # ------------------------------------------------------------------ encode
     @property
     def pending(self) -> int:
-        """Submits queued and not yet synced (at most 2)."""
+        """Submits queued and not yet synced (at most `depth`)."""
         return len(self._queued)
+
+    @property
+    def depth(self) -> int:
+        """Submits the library queues before one must be synced (mjg_queue_depth)."""
+        return int(self._L.mjg_queue_depth())
 
     def submit(self, frames=None, nframes: Optional[int] = None, device_ptr: Optional[int] = None):
         """Queue `nframes` packed frames: a host buffer (numpy / bytes) or a device pointer
-        (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU).  Two submits may be queued;
-        the second's k_encode runs beside the first's tail kernels (two streams)."""
+        (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU).  Up to `depth` submits may be
+        queued; each one's k_encode runs beside the previous one's drain and tail kernels."""
         if device_ptr is not None:
             if nframes is None:
                 raise ValueError("nframes is required with device_ptr")

@@ -124,10 +124,10 @@ size_t mjg_frame_bytes(const mjg_ctx *ctx);
 int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 
 /* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously: H2D, scale and
- * k_encode on the ctx stream, the scan/stuff/write tail on the ctx's second (tail) stream
- * after the submit's k_encode.  Up to two submits may be queued: the second one's k_encode
- * runs beside the first's tail (each has its own output and scratch buffers); MJG_E_STATE
- * with two queued.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
+ * k_encode on the submit's stream, the scan/stuff/write tail on the ctx's tail stream
+ * after the submit's k_encode.  Up to mjg_queue_depth() submits may be queued (each has its
+ * own output and scratch buffers and its own stream): the next one's k_encode runs beside the
+ * previous one's drain and tail; MJG_E_STATE with that many queued.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
  * staging buffer; pinned memory from mjg_host_alloc() makes this asynchronous);
  * src_is_device = 1: `frames` is device memory on ctx's device, read in place.
  * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
@@ -150,9 +150,11 @@ int mjg_fetch_host(mjg_ctx *ctx, const uint8_t **data, size_t *len);
  * entries, valid after mjg_sync). */
 int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offsets);
 /* The hipStream_t the next submit launches H2D, scale and k_encode on (for event timing by
- * the caller; the tail kernels run on another stream ordered after k_encode).  With
- * -huffman optimal or -vf scale consecutive submits alternate between two such streams. */
+ * the caller; the tail kernels run on another stream ordered after k_encode).  Consecutive
+ * submits rotate over mjg_queue_depth() such streams. */
 void *mjg_stream(mjg_ctx *ctx);
+/* How many submits mjg_submit queues before one must be synced (3). */
+int mjg_queue_depth(void);
 
 /* Pinned host memory for mjg_submit / mjg_fetch. */
 int mjg_host_alloc(size_t bytes, void **ptr);

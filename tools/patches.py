@@ -23,7 +23,7 @@ K = "kernels.hip"
 PATCHES = {
     # the stuffing tail on the submit stream: no co-run with the next submit's k_encode
     # (profiles/r03_ab_serial_tail.txt)
-    "serial_tail": lambda a: [("api.hip", "  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));\n",
+    "serial_tail": lambda a: [("api.hip", "  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, greatest));\n",
                                "  c->tail = c->stream;\n")],
     # no column skip test in the VALU column screen (profiles/r03_ab_column_skip.txt)
     "no_skip": lambda a: [(K, "    if (jp > 0 && (((st >> jp) & 1u) || retest)) {\n", "    if (false) {\n")],
@@ -156,10 +156,12 @@ PATCHES["prio_slot"] = lambda a: [(K, "  __syncthreads();  // tables visible; th
     "    if (slot == 3) __builtin_amdgcn_s_setprio(3);\n"
     "  }\n")]
 
-# default-table submits back to back on one stream (round 3's form; two streams since r04,
-# profiles/r04m_ab_two_streams_bench.txt)
-PATCHES["one_stream"] = lambda a: [("api.hip", "  S.st = &S == &c->slot[1] ? c->stream2 : c->stream;",
-                                    "  S.st = (&S == &c->slot[1] && (c->optimal || c->scale)) ? c->stream2 : c->stream;")]
+# every submit on one stream, back to back (round 3's form for default tables; a stream per
+# slot since r04, profiles/r04m_ab_two_streams_bench.txt)
+PATCHES["one_stream"] = lambda a: [("api.hip", "  S.st = slot_stream(c, (int)(&S - c->slot));", "  S.st = c->stream;")]
+# the submit queue three deep, a stream per slot (profiles/r04aa_depth_priority.txt: 10% slower,
+# three k_encode launches share the CUs)
+PATCHES["slots3"] = lambda a: [("api.hip", "constexpr int kSlots = 2;", "constexpr int kSlots = 3;")]
 
 # probes (wrong output): the stuffing tail's co-run cost on the bench (the kernels launch, and
 # return at once)
@@ -263,26 +265,12 @@ def _cpc_hybrid(a):
 PATCHES["cpc_hybrid"] = _cpc_hybrid
 
 
-# HIP stream priorities: the stuffing tail's stream at the lowest priority ("tail"), or also
-# both submit streams at the highest ("both"), so k_encode's workgroups dispatch first; or the
-# tail's stream at the highest ("tailhigh"), so a submit's slot is released sooner
-_STREAMS = ("  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));\n"
-            "  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));\n"
-            "  HIP_TRY(hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking));\n")
-
-
-def _stream_prio(a):
-    hi = "greatest" if a == "both" else "0"
-    tail = "greatest" if a == "tailhigh" else "least"
-    return [("api.hip", _STREAMS,
-             "  int least = 0, greatest = 0;\n"
-             "  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));\n"
-             f"  HIP_TRY(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, {hi}));\n"
-             f"  HIP_TRY(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, {hi}));\n"
-             f"  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, {tail}));\n")]
-
-
-PATCHES["stream_prio"] = _stream_prio
+# HIP stream priority of the stuffing tail's stream (the product: the highest, since r04;
+# profiles/r04s_ab_stream_priority.txt, r04z_ab_tail_high_priority.txt, r04aa_depth_priority.txt):
+# "low" = the lowest, "normal" = the default (rounds 1-4 until r04)
+PATCHES["stream_prio"] = lambda a: [("api.hip", "  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, greatest));\n",
+                                     "  HIP_TRY(hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, "
+                                     + {"low": "least", "normal": "0"}.get(a, "0") + "));\n")]
 
 
 # pack_chunk for every chunk, without pack_chunk_short's fast path for chunks of short blocks
