@@ -304,6 +304,12 @@ PATCHES["deposit_asm"] = lambda a: [(K, _DEPOSIT, """          const uint32_t sb
 """)]
 
 
+# the stuffing tail's wave priority (the product: kTailPrio = 2 since r04; before: 0).  They
+# share SIMDs with the next submit's k_encode waves, which the oldest-first arbiter otherwise
+# issues first (profiles/r04ad_tail_wave_priority.txt, r04ae_tail_wave_priority_levels.txt)
+PATCHES["tail_prio"] = lambda a: [(K, "constexpr int kTailPrio = 2;", f"constexpr int kTailPrio = {int(a) if a else 0};")]
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
