@@ -1668,13 +1668,21 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
 }
 
 // The stuffing tail's waves (k_scan_bits, k_count_ff, k_scan_ff, k_write) run at wave
-// priority 2.  They share SIMDs with the next submit's k_encode waves, which are older, and the
-// SIMD arbiter issues the oldest wave first: at priority 0 a submit's tail ended ~590 us after
-// its k_encode (~100 us of work), and the host, whose sync of that submit frees the slot the
-// submit after next reuses, waited for it.  At 2 it ends ~260 us after; c5 +14%, c4 +1%, c2
-// within noise, natural -1.3% (bench.py; profiles/r04ad_tail_wave_priority.txt,
-// r04ae_tail_wave_priority_levels.txt).
+// priority 2 when the submit's stream is light.  They share SIMDs with the next submit's
+// k_encode waves, which are older, and the SIMD arbiter issues the oldest wave first: at
+// priority 0 a submit's tail ended ~590 us after its k_encode (~100 us of work), and the host,
+// whose sync of that submit frees the slot the submit after next reuses, waited for it.  At 2
+// it ends ~260 us after; c5 +14%, c4 +1%, c2 within noise, but natural -1.3% (bench.py;
+// profiles/r04ad_tail_wave_priority.txt, r04ae_tail_wave_priority_levels.txt): a heavy stream's
+// tail (2-4x the bytes) then takes that much more issue from k_encode.  So the raise is kept to
+// submits whose first segment averages under kTailLightBits per chunk (BASELINE's testsrc
+// workloads 740-1440 bits, the fractal content 2190, noise-patches 3340).
 constexpr int kTailPrio = 2;
+constexpr uint32_t kTailLightBits = 1800;
+__device__ __forceinline__ void tail_priority(const uint32_t *seg_bits, int nchunks) {
+  if ((uint32_t)__builtin_amdgcn_readfirstlane((int)seg_bits[0]) < kTailLightBits * (uint32_t)nchunks)
+    __builtin_amdgcn_s_setprio(kTailPrio);
+}
 
 // --------------------------------------------------------------- block scan
 // Exclusive scan of n uint32 values with one 1024-thread workgroup; returns the total.
@@ -1931,7 +1939,7 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
                                                   uint32_t *__restrict__ group_ff, int nchunks, int gps,
                                                   int ngroups, uint32_t *__restrict__ stream) {
   __shared__ uint8_t s_marks[4][64 * kTailRounds];
-  __builtin_amdgcn_s_setprio(kTailPrio);
+  tail_priority(seg_bits, nchunks);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int gi = blockIdx.x * 4 + wave;  // wave-uniform: the group's pointers are scalar
   for (int i = lane; i < 64 * kTailRounds; i += 64) s_marks[wave][i] = 0;
@@ -1967,7 +1975,7 @@ __global__ __launch_bounds__(256) void k_scan_ff(const uint32_t *__restrict__ gr
                                                  uint32_t *__restrict__ seg_off, uint64_t *__restrict__ frame_size,
                                                  uint64_t *__restrict__ frame_offsets, uint32_t *__restrict__ done) {
   __shared__ uint32_t s_last;
-  __builtin_amdgcn_s_setprio(kTailPrio);
+  tail_priority(seg_bits, gps * kChunksPerWave);
   const int f = blockIdx.x, nframes = gridDim.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t mine = 0;  // nseg == 1: the segment's size (wave 0)
   for (int si = wave; si < nseg; si += 4) {
@@ -2078,7 +2086,7 @@ __global__ __launch_bounds__(256) void k_write(
     const uint32_t *__restrict__ dht_nval, uint8_t *__restrict__ out, uint64_t out_cap,
     uint32_t *__restrict__ status) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  __builtin_amdgcn_s_setprio(kTailPrio);
+  tail_priority(seg_bits, nchunks);
   const int gi = blockIdx.x * 4 + wave, ngroups = gps * nseg * nframes;
   if (gi >= ngroups) return;
   const int s = gi / gps, gx = gi - s * gps, f = s / nseg, si = s - f * nseg;

@@ -308,6 +308,8 @@ PATCHES["deposit_asm"] = lambda a: [(K, _DEPOSIT, """          const uint32_t sb
 # share SIMDs with the next submit's k_encode waves, which the oldest-first arbiter otherwise
 # issues first (profiles/r04ad_tail_wave_priority.txt, r04ae_tail_wave_priority_levels.txt)
 PATCHES["tail_prio"] = lambda a: [(K, "constexpr int kTailPrio = 2;", f"constexpr int kTailPrio = {int(a) if a else 0};")]
+# the raise for every submit, light or heavy (r04ad/r04ae's form)
+PATCHES["tail_prio_always"] = lambda a: [(K, "constexpr uint32_t kTailLightBits = 1800;", "constexpr uint32_t kTailLightBits = 0xffffffffu / 65536u;")]
 
 
 def parse_spec(spec: str):
