@@ -219,6 +219,30 @@ def _quad(a):
 PATCHES["quad"] = _quad
 
 
+def _quad_adaptive(a):
+    """emit_block's four-candidate form only for chunks where some per-lane block has more than
+    `a` candidates (natural content), the pair form elsewhere (testsrc)"""
+    src = open(os.path.join(CSRC, K)).read()
+    i = src.index("template <class Sink>\n__device__ __forceinline__ void emit_block(")
+    j = src.index("  if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB\n}\n", i) + len("  if (prev != 63) sink.ac(0x00, 0, 0u);  // EOB\n}\n")
+    body = src[i:j]
+    k0 = body.index(_PAIR_OLD)
+    k1 = body.index(_PAIR_END, k0) + len(_PAIR_END)
+    quad = body[:k0] + _QUAD + body[k1:]
+    quad = quad.replace("void emit_block(", "void emit_block4(")
+    call = "      emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);\n"
+    return [
+        (K, body, body + "\n" + quad),
+        (K, "    if (cur_active && !((wide >> lane) & 1ull)) {\n" + call,
+         f"    const bool quad_h = __ballot(cur_active && !((wide >> lane) & 1ull) && __popcll(mask) > {int(a)}) != 0ull;\n"
+         "    if (cur_active && !((wide >> lane) & 1ull)) {\n"
+         "      if (quad_h)\n  emit_block4(s_pk + lane, mask, diff, s_zd, s_m2, q);\n      else\n  " + call),
+    ]
+
+
+PATCHES["quad_adaptive"] = _quad_adaptive
+
+
 # the chunk-parallel coder prototype (tools/cpc_proto.hip) in place of the per-lane emission,
 # the wave-parallel blocks and pack_chunk
 _CPC_OLD_START = "    const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);\n"
