@@ -96,8 +96,9 @@ def load():
         L.mjg_output_device.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
         L.mjg_stream.argtypes = [vp]
         L.mjg_stream.restype = vp
-        L.mjg_queue_depth.argtypes = []
-        L.mjg_queue_depth.restype = C.c_int
+        if hasattr(L, "mjg_queue_depth"):  # absent from libraries built before r04 (A/B builds)
+            L.mjg_queue_depth.argtypes = []
+            L.mjg_queue_depth.restype = C.c_int
         L.mjg_host_alloc.argtypes = [sz, C.POINTER(vp)]
         L.mjg_host_free.argtypes = [vp]
         L.mjg_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_int]

@@ -144,7 +144,7 @@ class MjpegEncoder:
     @property
     def depth(self) -> int:
         """Submits the library queues before one must be synced (mjg_queue_depth)."""
-        return int(self._L.mjg_queue_depth())
+        return int(self._L.mjg_queue_depth()) if hasattr(self._L, "mjg_queue_depth") else 2
 
     def submit(self, frames=None, nframes: Optional[int] = None, device_ptr: Optional[int] = None):
         """Queue `nframes` packed frames: a host buffer (numpy / bytes) or a device pointer
