@@ -109,8 +109,12 @@ def load():
         L.mjg_build_header.argtypes = [C.POINTER(MjgConfig), u8p, sz, C.POINTER(sz)]
         L.mjg_sws_filter.argtypes = [C.c_int] * 7 + [C.POINTER(C.c_int16), sz, C.POINTER(C.c_int32),
                                                      C.POINTER(C.c_int)]
-        for name in EXPORTS:  # fail loudly on a stale / partial build
-            getattr(L, name)
+        # fail loudly on a stale / partial build (an A/B library from before r04 named by
+        # MJG_LIBRARY may lack mjg_queue_depth: the queue is then two deep)
+        late = ("mjg_queue_depth",) if os.environ.get("MJG_LIBRARY") else ()
+        for name in EXPORTS:
+            if name not in late:
+                getattr(L, name)
         _lib = L
         return L
 

@@ -336,6 +336,12 @@ PATCHES["tail_prio"] = lambda a: [(K, "constexpr int kTailPrio = 2;", f"constexp
 PATCHES["tail_prio_always"] = lambda a: [(K, "constexpr uint32_t kTailLightBits = 1800;", "constexpr uint32_t kTailLightBits = 0xffffffffu / 65536u;")]
 
 
+# -huffman optimal's counting pass launched with the default pass's grid (4 workgroups per CU,
+# of which 3 are resident: round 3's form) instead of its own occupancy
+PATCHES["count_grid_full"] = lambda a: [("api.hip", "    c->enc_grid_cnt = std::max(1, ncu * std::max(1, pc));\n",
+                                          "    c->enc_grid_cnt = c->enc_grid;\n")]
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
