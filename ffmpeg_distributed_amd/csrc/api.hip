@@ -793,12 +793,11 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       &per_cu, c->dct_mfma ? (const void *)k_encode<true, kEmitDefault, true> : (const void *)k_encode<true, kEmitDefault>,
       64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
+  // -huffman optimal's counting pass (per-wave histograms: 3 workgroups fit per CU) is launched
+  // with the same grid: the fourth workgroup of a CU starts as the first to finish leaves and
+  // pulls the units left; sized to its own occupancy it measured 1.8% slower on c1
+  // (profiles/r04an_c1_count_grid_tail_prio.txt)
   c->enc_grid_cnt = c->enc_grid;
-  if (c->optimal) {  // the per-wave histograms: fewer workgroups per CU (3 instead of 4)
-    int pc = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void *)k_encode<true, kCount>, 64 * kWavesPerWg, 0));
-    c->enc_grid_cnt = std::max(1, ncu * std::max(1, pc));
-  }
   size_t stage_cols = (size_t)c->enc_grid * kWavesPerWg;
   if (c->fused) {
     int fper = 0;

@@ -336,10 +336,12 @@ PATCHES["tail_prio"] = lambda a: [(K, "constexpr int kTailPrio = 2;", f"constexp
 PATCHES["tail_prio_always"] = lambda a: [(K, "constexpr uint32_t kTailLightBits = 1800;", "constexpr uint32_t kTailLightBits = 0xffffffffu / 65536u;")]
 
 
-# -huffman optimal's counting pass launched with the default pass's grid (4 workgroups per CU,
-# of which 3 are resident: round 3's form) instead of its own occupancy
-PATCHES["count_grid_full"] = lambda a: [("api.hip", "    c->enc_grid_cnt = std::max(1, ncu * std::max(1, pc));\n",
-                                          "    c->enc_grid_cnt = c->enc_grid;\n")]
+# -huffman optimal's counting pass sized to its own occupancy (3 workgroups per CU; r04 until
+# r04an) instead of the default pass's grid (profiles/r04an_c1_count_grid_tail_prio.txt)
+PATCHES["count_grid_own"] = lambda a: [("api.hip", "  c->enc_grid_cnt = c->enc_grid;\n",
+                                         "  c->enc_grid_cnt = c->enc_grid;\n  if (c->optimal) {\n    int pc = 0;\n"
+                                         "    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void *)k_encode<true, kCount>, 64 * kWavesPerWg, 0));\n"
+                                         "    c->enc_grid_cnt = std::max(1, ncu * std::max(1, pc));\n  }\n")]
 
 
 def parse_spec(spec: str):
