@@ -442,14 +442,16 @@ def test_rst_with_optimal_is_rejected():
 
 
 def test_pipelined_submits():
-    """Two submits queued at once (their kernels run back to back on the ctx stream, each
-    with its own scratch/output slot); sync completes them oldest first; a third queued
-    submit is refused; overflow regrowth works on a queued slot."""
+    """mjg_queue_depth() (2) submits queued at once (each with its own scratch/output slot and
+    stream); sync completes them oldest first; one more queued submit is refused; overflow
+    regrowth works on a queued slot.  A light stream (smooth) and a heavy one (noise at q=2)
+    take both branches of the stuffing tail's wave priority (kernels.hip tail_priority)."""
     from ffmpeg_distributed_amd._lib import MjgError
     w, h, q = 96, 64, 4
     frames = rand_frames(w, h, 7, seed=21, kind="smooth")
     ref = oracle_frames(frames, w, h, q, False)
     with MjpegEncoder(0, w, h, qscale=q, max_batch=3) as enc:
+        assert enc.depth == 2
         enc.submit(frames[0:3])
         enc.submit(frames[3:5])
         with pytest.raises(MjgError):
@@ -478,11 +480,10 @@ def test_pipelined_submits():
 
 @pytest.mark.parametrize("cfg", ["optimal", "scale", "scale_optimal", "default"])
 def test_pipelined_submits_two_streams(cfg):
-    """-huffman optimal and -vf scale contexts run their two slots on two streams (their
-    chains of launches overlap, csrc/api.hip alloc_slot; a default-table context keeps one
-    stream): five submits, two queued at a time so every slot is reused on its own stream, from
-    host memory (per-slot H2D staging) and with ragged batches; every frame byte-equal to the
-    oracle."""
+    """Every context runs its two slots on two streams (consecutive submits' launches overlap,
+    csrc/api.hip alloc_slot): five submits, two queued at a time so every slot is reused on its
+    own stream, from host memory (per-slot H2D staging) and with ragged batches; every frame
+    byte-equal to the oracle."""
     sw, sh = 200, 120
     dw, dh = (100, 60) if cfg.startswith("scale") else (sw, sh)
     huffman = "optimal" if cfg.endswith("optimal") else "default"
