@@ -344,6 +344,12 @@ PATCHES["count_grid_own"] = lambda a: [("api.hip", "  c->enc_grid_cnt = c->enc_g
                                          "    c->enc_grid_cnt = std::max(1, ncu * std::max(1, pc));\n  }\n")]
 
 
+# k_encode's persistent grid at N workgroups per CU below the occupancy (4): the launch leaves
+# CU slots free for the next submit's k_encode and for the tail
+PATCHES["enc_grid_per_cu"] = lambda a: [("api.hip", "  c->enc_grid = std::max(1, ncu * std::max(1, per_cu));\n",
+                                          f"  c->enc_grid = std::max(1, ncu * std::max(1, std::min(per_cu, {int(a) if a else 3})));\n")]
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
