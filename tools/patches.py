@@ -350,6 +350,29 @@ PATCHES["enc_grid_per_cu"] = lambda a: [("api.hip", "  c->enc_grid = std::max(1,
                                           f"  c->enc_grid = std::max(1, ncu * std::max(1, std::min(per_cu, {int(a) if a else 3})));\n")]
 
 
+# young waves (wave slot >= 2 on their SIMD: the oldest-first arbiter runs them ~2x slower) stop
+# taking units when fewer than (waves of the XCD) / D remain on their XCD, so the launch's last
+# units run on old waves and the drain is shorter; old waves still pull until every counter is dry
+def _young_exit(a):
+    d = int(a) if a else 2
+    return [
+        (K, """  __device__ __forceinline__ int next(uint32_t *ctr, int nwg) const {
+    for (int k = 0; k < NX; k++) {""", f"""  __device__ __forceinline__ int next(uint32_t *ctr, int nwg, bool young = false) const {{
+    if (young) {{
+      const int used = (int)__hip_atomic_load(ctr + j * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (start(j + 1) - (start(j) + nw(j, nwg) + used) < nw(j, nwg) / {d}) return nbatch;
+    }}
+    for (int k = 0; k < NX; k++) {{"""),
+        (K, "    if (t + 1 == tend && lane == 0) nb = (uint32_t)xu.next(work_ctr, nwg);",
+         "    if (t + 1 == tend && lane == 0) nb = (uint32_t)xu.next(work_ctr, nwg, young_w);"),
+        (K, "  const int nwg = gridDim.x;\n  int u0 = xu.start(xu.j)",
+         "  const int nwg = gridDim.x;\n  const bool young_w = NX > 1 && (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 15) >= 2;\n  int u0 = xu.start(xu.j)"),
+    ]
+
+
+PATCHES["young_exit"] = _young_exit
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
