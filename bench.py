@@ -415,7 +415,7 @@ def main():
                        dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
     bytes_out = []
 
-    # Segments are pipelined enc.depth (3) deep, as mjg_submit queues them: later segments'
+    # Segments are pipelined enc.depth (mjg_queue_depth(): 2) deep, as mjg_submit queues them: later segments'
     # kernels are queued behind segment s's before s is synced, so the GPU does not idle while
     # the host collects a segment's sizes and issues the next launches.
     depth = enc.depth
