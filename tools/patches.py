@@ -373,6 +373,73 @@ def _young_exit(a):
 PATCHES["young_exit"] = _young_exit
 
 
+# young waves (wave slot >= 2 on their SIMD) pull dynamic units of S chunks instead of kBatch,
+# so a unit takes about as long on a young wave as a full one on an old wave and the launch's
+# last units end closer together; the per-XCD counters count chunks instead of units
+# (S = kBatch: the same schedule as HEAD with chunk counters, a control)
+def _young_half(a):
+    s = int(a) if a else 6
+    return [
+        (K, """  // lane 0: the next unit (>= nbatch: none left)
+  __device__ __forceinline__ int next(uint32_t *ctr, int nwg) const {""",
+         """  // lane 0: chunks [p, e) of the next dynamic range of `size` chunks (p >= ntasks: none left)
+  __device__ __forceinline__ int next_c(uint32_t *ctr, int nwg, int size, int kb, int ntasks, int &e) const {
+    for (int k = 0; k < NX; k++) {
+      const int x = (j + k) & (NX - 1), ce = min(start(x + 1) * kb, ntasks);
+      const int p = (start(x) + nw(x, nwg)) * kb + (int)atomicAdd(ctr + x * kCtrStride, (uint32_t)size);
+      if (p < ce) {
+        e = min(p + size, ce);
+        return p;
+      }
+    }
+    return ntasks;
+  }
+  // lane 0: the next unit (>= nbatch: none left)
+  __device__ __forceinline__ int next(uint32_t *ctr, int nwg) const {"""),
+        (K, """  if (u0 >= xu.start(xu.j + 1)) {  // none: straight to the counters
+    int v = 0;
+    if (lane == 0) v = xu.next(work_ctr, nwg);
+    u0 = __builtin_amdgcn_readfirstlane(v);
+    if (u0 >= nbatch) return;
+  }""", f"""  const bool young_w = NX > 1 && (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 15) >= 2;
+  const int usz = young_w ? {s} : kBatch;
+  int t0 = u0 * kBatch, te0 = min(t0 + kBatch, ntasks);
+  if (u0 >= xu.start(xu.j + 1)) {{  // none: straight to the counters
+    int v = 0, ve = 0;
+    if (lane == 0) v = xu.next_c(work_ctr, nwg, usz, kBatch, ntasks, ve);
+    t0 = __builtin_amdgcn_readfirstlane(v);
+    te0 = __builtin_amdgcn_readfirstlane(ve);
+    if (t0 >= ntasks) return;
+  }}"""),
+        (K, "  int t = u0 * kBatch, tend = min(t + kBatch, ntasks);\n  uint32_t nb = 0;",
+         "  int t = t0, tend = te0;\n  uint32_t nb = 0, nbe = 0;"),
+        (K, "    if (t + 1 == tend && lane == 0) nb = (uint32_t)xu.next(work_ctr, nwg);",
+         """    if (t + 1 == tend && lane == 0) {
+      int e_ = 0;
+      nb = (uint32_t)xu.next_c(work_ctr, nwg, usz, kBatch, ntasks, e_);
+      nbe = (uint32_t)e_;
+    }"""),
+        (K, """    const bool new_batch = tn >= tend;
+    if (new_batch) {
+      const int nbu = __builtin_amdgcn_readfirstlane(nb);
+      tn = nbu < nbatch ? nbu * kBatch : -1;
+    }""", """    const bool new_batch = tn >= tend;
+    int nend = 0;
+    if (new_batch) {
+      const int nbu = __builtin_amdgcn_readfirstlane(nb);
+      tn = nbu < ntasks ? nbu : -1;
+      nend = __builtin_amdgcn_readfirstlane(nbe);
+    }"""),
+        (K, "carry = carry_finish(crow, chunk, lane, rc, g, s_desc);\n        tend = min(tn + kBatch, ntasks);",
+         "carry = carry_finish(crow, chunk, lane, rc, g, s_desc);\n        tend = nend;"),
+        (K, "carry = carry_finish(crow, chunk, lane, rc, g, s_desc);\n      tend = min(tn + kBatch, ntasks);",
+         "carry = carry_finish(crow, chunk, lane, rc, g, s_desc);\n      tend = nend;"),
+    ]
+
+
+PATCHES["young_half"] = _young_half
+
+
 def parse_spec(spec: str):
     """'no_skip+wide_cost=3' -> [('no_skip', None), ('wide_cost', '3')]"""
     out = []
