@@ -69,6 +69,8 @@ def parse():
                    help="internal: run the CPU baseline sweep alone (no torch, no GPU) and print it")
     p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (rank 0, N=1 only)")
     p.add_argument("--e2e-segments", type=int, default=6)
+    p.add_argument("--no-batched", action="store_true",
+                   help="skip the multi-segment-submit leg (mjg_submit_segments, N=1 only)")
     p.add_argument("--fused", action="store_true",
                    help="-vf scale configs: the opt-in fused k_scale_encode instead of k_scale + k_encode")
     p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
@@ -131,6 +133,44 @@ def _cpu_encode_until(args):
         n += 1
         if time.time() >= deadline:
             return n, nbytes, time.time()
+
+
+def segments_per_launch(a, pool, seg, nseg_pool, W, H, FULL, Q, HUFF, device, ks=(2, 4), nsegs=240):
+    """Reported beside the headline, not as it: the same segments handed over K per submit
+    (mjg_submit_segments; one k_encode launch and one tail per K segments, each segment's
+    bytes those of its own submit).  The headline stays one segment per submit, which is what
+    the per-segment worker path (fd.py:139-141 once per segment) does today."""
+    import torch
+    from ffmpeg_distributed_amd.encoder import MjpegEncoder
+    res = {}
+    for k in ks:
+        if k > nseg_pool:
+            continue
+        enc = MjpegEncoder(device, W, H, W, H, full_range=FULL, qscale=Q, max_batch=k * seg,
+                           huffman=HUFF)
+        if k > enc.max_segments:
+            enc.close()
+            continue
+        ptrs = [pool[j * seg].data_ptr() for j in range(nseg_pool)]
+
+        def run(n, s0):
+            for s in range(s0, s0 + n):
+                enc.submit_segments([(ptrs[(s * k + i) % nseg_pool], seg) for i in range(k)])
+                if enc.pending == enc.depth:
+                    enc.sync()
+            while enc.pending:
+                enc.sync()
+            torch.cuda.synchronize()
+        steps = max(8, nsegs // k)  # ~240 segments per K: the pipeline's fill and drain are <1%
+        run(4, 0)
+        t0 = time.perf_counter()
+        run(steps, 4)
+        dt = time.perf_counter() - t0
+        enc.close()
+        res[str(k)] = {"value": round(steps * k * seg / dt, 2), "unit": "frames/s",
+                       "ms_per_segment": round(dt / (steps * k) * 1e3, 4),
+                       "segments_per_submit": k, "submits": steps}
+    return res
 
 
 def cpu_baseline_sweep(seconds: float):
@@ -455,6 +495,10 @@ def main():
                                     dt / a.steps * 1e3 if overlap else None)
     primary = dict(primary, launches=nl, traffic_source=pmc_src)
 
+    batched = None
+    if not a.no_batched and world == 1 and (DW, DH) == (W, H) and not a.fused and not a.rst and nseg_pool >= 2:
+        batched = segments_per_launch(a, pool, seg, nseg_pool, W, H, FULL, Q, HUFF, local)
+
     out = None
     if rank == 0:
         e2e_res = None
@@ -501,6 +545,7 @@ def main():
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},
             "mean_jpeg_bytes": round(mean_jpeg, 1),
             "e2e": e2e_res,
+            "segments_per_launch": batched,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

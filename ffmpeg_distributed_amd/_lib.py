@@ -41,7 +41,7 @@ MJG_NUM_KERNELS = len(KERNEL_NAMES)
 EXPORTS = (
     "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_device_numa_node", "mjg_open", "mjg_close",
     "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch", "mjg_fetch_host",
-    "mjg_output_device", "mjg_stream", "mjg_queue_depth", "mjg_host_alloc", "mjg_host_free",
+    "mjg_output_device", "mjg_stream", "mjg_queue_depth", "mjg_submit_segments", "mjg_max_segments", "mjg_host_alloc", "mjg_host_free",
     "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
     "mjg_debug_planes", "mjg_debug_filter",
 )
@@ -99,6 +99,10 @@ def load():
         if hasattr(L, "mjg_queue_depth"):  # absent from libraries built before r04 (A/B builds)
             L.mjg_queue_depth.argtypes = []
             L.mjg_queue_depth.restype = C.c_int
+        if hasattr(L, "mjg_submit_segments"):  # absent from libraries built before r04 (A/B builds)
+            L.mjg_submit_segments.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_int), C.c_int]
+            L.mjg_max_segments.argtypes = []
+            L.mjg_max_segments.restype = C.c_int
         L.mjg_host_alloc.argtypes = [sz, C.POINTER(vp)]
         L.mjg_host_free.argtypes = [vp]
         L.mjg_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_int]
@@ -110,8 +114,10 @@ def load():
         L.mjg_sws_filter.argtypes = [C.c_int] * 7 + [C.POINTER(C.c_int16), sz, C.POINTER(C.c_int32),
                                                      C.POINTER(C.c_int)]
         # fail loudly on a stale / partial build (an A/B library from before r04 named by
-        # MJG_LIBRARY may lack mjg_queue_depth: the queue is then two deep)
-        late = ("mjg_queue_depth",) if os.environ.get("MJG_LIBRARY") else ()
+        # MJG_LIBRARY may lack mjg_queue_depth: the queue is then two deep; and the
+        # multi-segment submit, which only bench.py's segments_per_launch leg calls)
+        late = (("mjg_queue_depth", "mjg_submit_segments", "mjg_max_segments")
+                if os.environ.get("MJG_LIBRARY") else ())
         for name in EXPORTS:
             if name not in late:
                 getattr(L, name)

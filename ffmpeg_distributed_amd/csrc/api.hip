@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -860,7 +861,7 @@ void launch_fused(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
 }
 
 template <int MODE, bool MF, bool DBG>
-void launch_encode3(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+void launch_encode3(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
   if (g.range_convert)
     k_encode<true, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
@@ -873,7 +874,7 @@ void launch_encode3(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int nta
 }
 
 template <int MODE, bool MF>
-void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+void launch_encode2(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
   if (c->geom.debug_coefs)
     launch_encode3<MODE, MF, true>(c, S, enc_in, wgs, ntasks);
   else
@@ -882,7 +883,7 @@ void launch_encode2(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int nta
 
 // The DCT stage: the VALU passes, or (-huffman default) dct_mfma.
 template <int MODE>
-void launch_encode(mjg_ctx *c, Slot &S, const uint8_t *enc_in, int wgs, int ntasks) {
+void launch_encode(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
   if (MODE == kEmitDefault && c->dct_mfma)
     launch_encode2<kEmitDefault, true>(c, S, enc_in, wgs, ntasks);
   else
@@ -945,8 +946,10 @@ int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len) {
   return MJG_OK;
 }
 
-int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
-  if (!c || !frames) return set_err(MJG_E_INVALID, "null argument");
+namespace {
+// mjg_submit's body; segs (mjg_submit_segments: device frames, no -vf scale) replaces the one
+// segment at `frames` as k_encode's input
+int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, const SegList *segs) {
   if (n < 1 || n > c->cfg.max_batch)
     return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
   if (c->nout == kSlots) return set_err(MJG_E_STATE, "%d submits queued: sync one first", kSlots);
@@ -966,7 +969,7 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     HIP_TRY(hipMemcpyAsync(S.d_stage, frames, (size_t)n * c->in_frame_bytes, hipMemcpyHostToDevice, S.st));
     src = S.d_stage;
   }
-  const uint8_t *enc_in = src;
+  const uint8_t *scaled_in = src;
   if (c->scale && !c->fused) {
     tmark(c, S, MJG_K_SCALE, 0);
     const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
@@ -1022,7 +1025,16 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
     }
     tmark(c, S, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());
-    enc_in = S.d_scaled;
+    scaled_in = S.d_scaled;
+  }
+  SegList enc_in;
+  if (segs) {
+    enc_in = *segs;
+  } else {
+    for (int k = 0; k < kMaxSegs; k++) {
+      enc_in.p[k] = scaled_in;
+      enc_in.f0[k] = k ? INT_MAX : 0;
+    }
   }
   const int ntasks = g.nchunks * g.nseg * n;
   const int nsegs = g.nseg * n;  // entropy-coded segments of this submit
@@ -1086,6 +1098,35 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   c->nout++;
   c->synced_since_submit = false;
   return MJG_OK;
+}
+}  // namespace
+
+int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
+  if (!c || !frames) return set_err(MJG_E_INVALID, "null argument");
+  return submit_impl(c, frames, n, src_is_device, nullptr);
+}
+
+int mjg_max_segments(void) { return kMaxSegs; }
+
+int mjg_submit_segments(mjg_ctx *c, const uint8_t *const *seg_frames, const int *seg_nframes, int nsegs) {
+  if (!c || !seg_frames || !seg_nframes) return set_err(MJG_E_INVALID, "null argument");
+  if (nsegs < 1 || nsegs > kMaxSegs) return set_err(MJG_E_INVALID, "nsegs %d not in 1..%d", nsegs, kMaxSegs);
+  if (c->scale) return set_err(MJG_E_INVALID, "multi-segment submits need a profile without -vf scale");
+  SegList sl;
+  int n = 0;
+  for (int k = 0; k < kMaxSegs; k++) {
+    if (k < nsegs) {
+      if (!seg_frames[k] || seg_nframes[k] < 1 || seg_nframes[k] > c->cfg.max_batch)
+        return set_err(MJG_E_INVALID, "segment %d: null frames or nframes not in 1..%d", k, c->cfg.max_batch);
+      sl.p[k] = seg_frames[k];
+      sl.f0[k] = n;
+      n += seg_nframes[k];
+    } else {
+      sl.p[k] = seg_frames[0];
+      sl.f0[k] = INT_MAX;
+    }
+  }
+  return submit_impl(c, seg_frames[0], n, 1, &sl);
 }
 
 // Completes the oldest queued submit (or, with none queued, reports the last synced one).

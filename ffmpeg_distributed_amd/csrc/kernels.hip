@@ -90,6 +90,27 @@ struct EncGeom {
   int debug_coefs;
 };
 
+// A submit's input frames as up to kMaxSegs segments (mjg_submit_segments): segment k holds
+// the submit's frames [f0[k], f0[k + 1]) at p[k], frame_stride apart; unused entries have
+// f0 = INT_MAX.  One launch then covers several segments, so their ramp and drain are paid
+// once (DESIGN §4 segments).  A kernel argument, resolved with scalar selects per chunk.
+constexpr int kMaxSegs = 4;
+struct SegList {
+  const uint8_t *p[kMaxSegs];
+  int f0[kMaxSegs];
+};
+__device__ __forceinline__ const uint8_t *seg_frame(const SegList &sl, int f, long long stride) {
+  const uint8_t *b = sl.p[0];
+  int s0 = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxSegs; k++)
+    if (f >= sl.f0[k]) {
+      b = sl.p[k];
+      s0 = sl.f0[k];
+    }
+  return b + (size_t)(f - s0) * stride;
+}
+
 // block descriptor word: bits 0-1 plane, 2 Huffman table (chroma), 3 dx (8 px), 4 dy (8 px),
 // 8-11 distance to the previous block of the same component in coding order
 __device__ __forceinline__ int desc_tab(uint32_t d) { return (int)((d >> 2) & 1u); }
@@ -1162,7 +1183,7 @@ struct XcdUnits {
 // neither its branch nor its live scalars (k_encode is short of SGPRs: they spill to VGPR lanes).
 template <bool RC, int MODE, bool MF = false, bool DBG = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
-    const uint8_t *__restrict__ frames, EncGeom g, const uint32_t *__restrict__ tabs,
+    const SegList frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
     uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all,
@@ -1243,7 +1264,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   int b = chunk * 64 + lane;  // block in the segment
   bool active = b < nblk;
   // the chunk's frame base (wave-uniform) and whether it is 8-byte aligned
-  auto frame_base = [&](int f) { return frames + (size_t)f * g.frame_stride; };
+  auto frame_base = [&](int f) { return seg_frame(frames, f, g.frame_stride); };
   const uint8_t *fb = frame_base(frame);
   uint64_t raw[8];
   bool fast = fetch_rows(raw, fb, ((uintptr_t)fb & 7) == 0, block_pos(g, bbase + b, s_bd), active);

@@ -168,6 +168,24 @@ class MjpegEncoder:
         self._queued.append((n, arr))  # the async H2D copy reads arr until its sync
         self._synced_since_submit = False
 
+    def submit_segments(self, segments):
+        """Queue several segments as ONE submit (mjg_submit_segments): `segments` is a list of
+        (device_ptr, nframes) on this GPU, at most mjg_max_segments() of them, totalling at
+        most max_batch frames; profiles without -vf scale.  One k_encode launch covers them
+        all; sync() then returns the frames' sizes in segment order and fetch() their JPEGs,
+        the same bytes as one submit() per segment."""
+        k = len(segments)
+        ptrs = (C.c_void_p * max(k, 1))(*[C.c_void_p(int(p)) for p, _ in segments])
+        ns = (C.c_int * max(k, 1))(*[int(n) for _, n in segments])
+        check(self._L.mjg_submit_segments(self._h, ptrs, ns, k))
+        self._queued.append((sum(int(n) for _, n in segments), None))
+        self._synced_since_submit = False
+
+    @property
+    def max_segments(self) -> int:
+        """Most segments one submit_segments() may carry (mjg_max_segments)."""
+        return int(self._L.mjg_max_segments())
+
     def sync(self) -> np.ndarray:
         """Complete the oldest queued submit; its per-frame JPEG sizes."""
         if not self._queued:

@@ -132,6 +132,16 @@ int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
  * src_is_device = 1: `frames` is device memory on ctx's device, read in place.
  * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
 int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
+/* Several segments in one submit: segment k's seg_nframes[k] packed I420 frames at device
+ * pointer seg_frames[k] (on ctx's device), nsegs in 1..mjg_max_segments(), the total within
+ * max_batch; profiles without -vf scale.  One k_encode launch (and one tail) then covers all
+ * of them, so the launch's ramp and drain are paid once; the output is the frames in segment
+ * order, exactly the bytes of one mjg_submit per segment.  The resident encoder / a GPU worker
+ * with several segments queued on one GPU (ffmpeg_distributed.py:139-141 once per segment)
+ * hands them over together. */
+int mjg_submit_segments(mjg_ctx *ctx, const uint8_t *const *seg_frames, const int *seg_nframes, int nsegs);
+/* Most segments one mjg_submit_segments() may carry (4). */
+int mjg_max_segments(void);
 /* Wait for the oldest queued submit (with none queued: report the last synced one again).
  * frame_sizes (may be NULL) receives its nframes JPEG sizes; *total (may be NULL) the packed
  * total.  Grows the output buffer and re-runs the final kernel if the packed output
@@ -153,7 +163,7 @@ int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offse
  * the caller; the tail kernels run on another stream ordered after k_encode).  Consecutive
  * submits rotate over mjg_queue_depth() such streams. */
 void *mjg_stream(mjg_ctx *ctx);
-/* How many submits mjg_submit queues before one must be synced (3). */
+/* How many submits mjg_submit queues before one must be synced (2). */
 int mjg_queue_depth(void);
 
 /* Pinned host memory for mjg_submit / mjg_fetch. */

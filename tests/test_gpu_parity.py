@@ -341,6 +341,87 @@ def test_4k_segment_batch_from_device_memory():
     assert list(s1) == [len(r) for r in ref[60:]] and b == ref[60:]
 
 
+@pytest.mark.parametrize("w,h,full,huff", [(72, 40, False, "default"), (333, 177, True, "default"),
+                                            (1920, 1080, False, "optimal")])
+def test_submit_segments_matches_oracle(w, h, full, huff):
+    """mjg_submit_segments: three segments of 3, 1 and 4 frames in separate device buffers
+    as ONE submit (one k_encode launch); every frame byte-equal to the oracle, in segment
+    order, and the same bytes again from a second queued multi-segment submit."""
+    import torch
+    dev = torch.device("cuda", 0)
+    counts = [3, 1, 4]
+    frames = np.stack([make_testsrc(w, h, 7 * t + 3, full_range=full) for t in range(sum(counts))])
+    segs, o = [], 0
+    for k in counts:  # separate allocations: the segments are not contiguous in memory
+        segs.append(torch.from_numpy(frames[o:o + k].copy()).to(dev))
+        o += k
+    torch.cuda.synchronize()
+    ref = _oracle_many(frames, w, h, qscale=5, full_range=full, huffman=huff)
+    with MjpegEncoder(0, w, h, qscale=5, full_range=full, max_batch=sum(counts), huffman=huff) as enc:
+        assert enc.max_segments >= len(counts)
+        enc.submit_segments([(t.data_ptr(), t.shape[0]) for t in segs])
+        enc.submit_segments([(segs[2].data_ptr(), 4), (segs[0].data_ptr(), 3)])
+        s0 = enc.sync()
+        a = enc.fetch()
+        s1 = enc.sync()
+        b = enc.fetch()
+    assert list(s0) == [len(r) for r in ref]
+    for i in range(len(ref)):
+        assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
+    assert b == ref[4:] + ref[:3] and list(s1) == [len(r) for r in b]
+
+
+def test_4k_submit_segments_equals_per_segment_submits():
+    """BASELINE configs[1]'s segments (120 4K frames) two per submit: the bytes of each are
+    those of one submit per segment (which test_4k_segment_batch_from_device_memory pins to
+    the oracle), with two multi-segment submits queued."""
+    import torch
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    w, h, n = 3840, 2160, 120
+    dev = torch.device("cuda", 0)
+    pools = []
+    for j in range(3):
+        p = torch.empty((n, i420_frame_bytes(w, h)), dtype=torch.uint8, device=dev)
+        for i in range(0, n, 20):
+            p[i:i + 20] = testsrc2_i420_torch(w, h, 2000 + j * n + i, 20, dev)
+        pools.append(p)
+    torch.cuda.synchronize()
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=2 * n) as enc:
+        per = []
+        for p in pools:
+            enc.submit(device_ptr=p.data_ptr(), nframes=n)
+            enc.sync()
+            per.append(enc.fetch())
+        enc.submit_segments([(pools[0].data_ptr(), n), (pools[1].data_ptr(), n)])
+        enc.submit_segments([(pools[2].data_ptr(), n), (pools[0].data_ptr(), 60)])
+        enc.sync()
+        a = enc.fetch()
+        enc.sync()
+        b = enc.fetch()
+    assert a == per[0] + per[1]
+    assert b == per[2] + per[0][:60]
+
+
+def test_submit_segments_rejects_bad_lists():
+    """Errors, not undefined behaviour: no segments, more than mjg_max_segments(), a total
+    over max_batch, an empty segment, and a -vf scale profile."""
+    import torch
+    from ffmpeg_distributed_amd._lib import MjgError
+    w, h = 64, 48
+    t = torch.zeros((4, i420_frame_bytes(w, h)), dtype=torch.uint8, device="cuda:0")
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=4) as enc:
+        k = enc.max_segments
+        for bad in ([], [(t.data_ptr(), 1)] * (k + 1), [(t.data_ptr(), 3), (t.data_ptr(), 2)],
+                    [(t.data_ptr(), 0)]):
+            with pytest.raises(MjgError):
+                enc.submit_segments(bad)
+        enc.submit_segments([(t.data_ptr(), 2), (t.data_ptr(), 2)])  # still usable
+        assert len(enc.sync()) == 4
+    with MjpegEncoder(0, w, h, 32, 24, qscale=5, max_batch=4) as enc:
+        with pytest.raises(MjgError):
+            enc.submit_segments([(t.data_ptr(), 1)])
+
+
 def test_8k_yuvj420p_matches_oracle():
     """BASELINE configs[4]: 7680x4320 yuvj420p q=5 (no range conversion), every frame of a
     3-frame batch (and a ragged second submit) byte-equal to the oracle."""
