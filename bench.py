@@ -69,8 +69,9 @@ def parse():
                    help="internal: run the CPU baseline sweep alone (no torch, no GPU) and print it")
     p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (rank 0, N=1 only)")
     p.add_argument("--e2e-segments", type=int, default=6)
-    p.add_argument("--no-batched", action="store_true",
-                   help="skip the multi-segment-submit leg (mjg_submit_segments, N=1 only)")
+    p.add_argument("--segments-per-launch", action="store_true",
+                   help="also time K = 2, 4 segments per submit (mjg_submit_segments, N=1 only); off by "
+                        "default so a profile of the default command holds only the headline's launches")
     p.add_argument("--fused", action="store_true",
                    help="-vf scale configs: the opt-in fused k_scale_encode instead of k_scale + k_encode")
     p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
@@ -496,7 +497,7 @@ def main():
     primary = dict(primary, launches=nl, traffic_source=pmc_src)
 
     batched = None
-    if not a.no_batched and world == 1 and (DW, DH) == (W, H) and not a.fused and not a.rst and nseg_pool >= 2:
+    if a.segments_per_launch and world == 1 and (DW, DH) == (W, H) and not a.fused and not a.rst and nseg_pool >= 2:
         batched = segments_per_launch(a, pool, seg, nseg_pool, W, H, FULL, Q, HUFF, local)
 
     out = None
