@@ -402,6 +402,24 @@ def test_4k_submit_segments_equals_per_segment_submits():
     assert b == per[2] + per[0][:60]
 
 
+@pytest.mark.parametrize("chroma,rst", [("420", True), ("422", False), ("444", True)])
+def test_submit_segments_rst_and_chroma_match_oracle(chroma, rst):
+    """mjg_submit_segments with the RST layout (one entropy-coded segment per MCU row) and
+    4:2:2 / 4:4:4 input: two segments of 2 and 1 frames, byte-equal to the oracle."""
+    import torch
+    w, h, q = 200, 72, 4
+    frames = rand_frames(w, h, 3, seed=w + h + len(chroma), kind="smooth", chroma=chroma)
+    segs = [torch.from_numpy(frames[:2].copy()).to("cuda:0"), torch.from_numpy(frames[2:].copy()).to("cuda:0")]
+    torch.cuda.synchronize()
+    with MjpegEncoder(0, w, h, qscale=q, full_range=True, max_batch=3, chroma=chroma, rst=rst) as enc:
+        enc.submit_segments([(t.data_ptr(), t.shape[0]) for t in segs])
+        enc.sync()
+        got = enc.fetch()
+    ref = oracle_frames(frames, w, h, q, True, chroma=chroma, rst=rst)
+    for i in range(3):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
 def test_submit_segments_rejects_bad_lists():
     """Errors, not undefined behaviour: no segments, more than mjg_max_segments(), a total
     over max_batch, an empty segment, and a -vf scale profile."""
