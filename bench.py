@@ -136,7 +136,7 @@ def _cpu_encode_until(args):
             return n, nbytes, time.time()
 
 
-def segments_per_launch(a, pool, seg, nseg_pool, W, H, FULL, Q, HUFF, device, ks=(2, 4), nsegs=240):
+def segments_per_launch(a, pool, seg, nseg_pool, W, H, DW, DH, FULL, Q, HUFF, device, ks=(2, 4), nsegs=240):
     """Reported beside the headline, not as it: the same segments handed over K per submit
     (mjg_submit_segments; one k_encode launch and one tail per K segments, each segment's
     bytes those of its own submit).  The headline stays one segment per submit, which is what
@@ -147,7 +147,7 @@ def segments_per_launch(a, pool, seg, nseg_pool, W, H, FULL, Q, HUFF, device, ks
     for k in ks:
         if k > nseg_pool:
             continue
-        enc = MjpegEncoder(device, W, H, W, H, full_range=FULL, qscale=Q, max_batch=k * seg,
+        enc = MjpegEncoder(device, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=k * seg,
                            huffman=HUFF)
         if k > enc.max_segments:
             enc.close()
@@ -497,8 +497,8 @@ def main():
     primary = dict(primary, launches=nl, traffic_source=pmc_src)
 
     batched = None
-    if a.segments_per_launch and world == 1 and (DW, DH) == (W, H) and not a.fused and not a.rst and nseg_pool >= 2:
-        batched = segments_per_launch(a, pool, seg, nseg_pool, W, H, FULL, Q, HUFF, local)
+    if a.segments_per_launch and world == 1 and not a.fused and not a.rst and nseg_pool >= 2:
+        batched = segments_per_launch(a, pool, seg, nseg_pool, W, H, DW, DH, FULL, Q, HUFF, local)
 
     out = None
     if rank == 0:

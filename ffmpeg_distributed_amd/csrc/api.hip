@@ -969,7 +969,16 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
     HIP_TRY(hipMemcpyAsync(S.d_stage, frames, (size_t)n * c->in_frame_bytes, hipMemcpyHostToDevice, S.st));
     src = S.d_stage;
   }
-  const uint8_t *scaled_in = src;
+  SegList in_sl;  // the submit's input frames: the caller's segments, or one at src
+  if (segs) {
+    in_sl = *segs;
+  } else {
+    for (int k = 0; k < kMaxSegs; k++) {
+      in_sl.p[k] = src;
+      in_sl.f0[k] = k ? INT_MAX : 0;
+    }
+  }
+  SegList enc_in = in_sl;
   if (c->scale && !c->fused) {
     tmark(c, S, MJG_K_SCALE, 0);
     const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
@@ -994,13 +1003,13 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
 #define MJG_SCALE_LAUNCH3(HT, NPV, D4, TH)                                                          \
   do {                                                                                              \
     if (sg.range == 1)                                                                              \
-      k_scale<HT, NPV, D4, 1, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(src, S.d_scaled, sg, ps.hcp,        \
+      k_scale<HT, NPV, D4, 1, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(in_sl, S.d_scaled, sg, ps.hcp,        \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
     else if (sg.range == 2)                                                                         \
-      k_scale<HT, NPV, D4, 2, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(src, S.d_scaled, sg, ps.hcp,        \
+      k_scale<HT, NPV, D4, 2, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(in_sl, S.d_scaled, sg, ps.hcp,        \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
     else                                                                                            \
-      k_scale<HT, NPV, D4, 0, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(src, S.d_scaled, sg, ps.hcp,        \
+      k_scale<HT, NPV, D4, 0, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(in_sl, S.d_scaled, sg, ps.hcp,        \
                                                                     ps.hp, ps.vcp, ps.vps, ps.hsum); \
   } while (0)
 #define MJG_SCALE_LAUNCH(HT, NPV, TH)      \
@@ -1025,14 +1034,8 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
     }
     tmark(c, S, MJG_K_SCALE, 1);
     HIP_TRY(hipGetLastError());
-    scaled_in = S.d_scaled;
-  }
-  SegList enc_in;
-  if (segs) {
-    enc_in = *segs;
-  } else {
-    for (int k = 0; k < kMaxSegs; k++) {
-      enc_in.p[k] = scaled_in;
+    for (int k = 0; k < kMaxSegs; k++) {  // k_encode reads the scaled frames, one buffer
+      enc_in.p[k] = S.d_scaled;
       enc_in.f0[k] = k ? INT_MAX : 0;
     }
   }
@@ -1111,7 +1114,7 @@ int mjg_max_segments(void) { return kMaxSegs; }
 int mjg_submit_segments(mjg_ctx *c, const uint8_t *const *seg_frames, const int *seg_nframes, int nsegs) {
   if (!c || !seg_frames || !seg_nframes) return set_err(MJG_E_INVALID, "null argument");
   if (nsegs < 1 || nsegs > kMaxSegs) return set_err(MJG_E_INVALID, "nsegs %d not in 1..%d", nsegs, kMaxSegs);
-  if (c->scale) return set_err(MJG_E_INVALID, "multi-segment submits need a profile without -vf scale");
+  if (c->fused) return set_err(MJG_E_INVALID, "multi-segment submits: not with the opt-in fused scale kernel");
   SegList sl;
   int n = 0;
   for (int k = 0; k < kMaxSegs; k++) {

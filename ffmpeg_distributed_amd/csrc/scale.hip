@@ -110,7 +110,7 @@ typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 // HT / NPV: compile-time tap counts for the common filters (0 = runtime, any ratio); TH: tile
 // height (64 only with HT 8, NPV 5)
 template <int HT, int NPV, bool D4, int RANGE, int TH>  // RANGE: g.range as a compile-time value
-__global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const SegList src,  // the submit's input frames (kernels.hip)
                                                uint8_t *__restrict__ dst, ScaleGeom g,
                                                const int32_t *__restrict__ hcp,   // [dw][htaps/2]
                                                const int32_t *__restrict__ hp,    // [dw]
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const uint8_t *_
   }
   const int x0 = bx * kScaleTileW, y0 = by * TH;
   const int pl = z >= g.nf, f = z - (pl ? g.nf : 0);
-  const uint8_t *s = src + (size_t)f * g.s_fstride + g.s_off + (pl ? g.s_poff : 0);
+  const uint8_t *s = seg_frame(src, f, g.s_fstride) + g.s_off + (pl ? g.s_poff : 0);
   uint8_t *d = dst + (size_t)f * g.d_fstride + g.d_off + (pl ? g.d_poff : 0);
   const int xe = min(x0 + kScaleTileW, g.dw), ye = min(y0 + TH, g.dh);
   const int p0 = vps[y0], p1 = vps[ye - 1] + g.npv;  // row pairs [p0, p1)

@@ -171,7 +171,7 @@ class MjpegEncoder:
     def submit_segments(self, segments):
         """Queue several segments as ONE submit (mjg_submit_segments): `segments` is a list of
         (device_ptr, nframes) on this GPU, at most mjg_max_segments() of them, totalling at
-        most max_batch frames; profiles without -vf scale.  One k_encode launch covers them
+        most max_batch frames; not with fused=True.  One launch per kernel covers them
         all; sync() then returns the frames' sizes in segment order and fetch() their JPEGs,
         the same bytes as one submit() per segment."""
         k = len(segments)

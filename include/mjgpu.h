@@ -134,7 +134,7 @@ int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
 /* Several segments in one submit: segment k's seg_nframes[k] packed I420 frames at device
  * pointer seg_frames[k] (on ctx's device), nsegs in 1..mjg_max_segments(), the total within
- * max_batch; profiles without -vf scale.  One k_encode launch (and one tail) then covers all
+ * max_batch; not with MJG_F_FUSED.  One launch of each kernel (k_scale, k_encode, the tail) covers all
  * of them, so the launch's ramp and drain are paid once; the output is the frames in segment
  * order, exactly the bytes of one mjg_submit per segment.  The resident encoder / a GPU worker
  * with several segments queued on one GPU (ffmpeg_distributed.py:139-141 once per segment)

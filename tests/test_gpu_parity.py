@@ -420,9 +420,27 @@ def test_submit_segments_rst_and_chroma_match_oracle(chroma, rst):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
+@pytest.mark.parametrize("w,h,dw,dh,q", [(640, 360, 320, 180, 3), (330, 190, 500, 260, 5)])
+def test_submit_segments_scaled_match_oracle(w, h, dw, dh, q):
+    """-vf scale with segments (k_scale reads each segment's frames from its own buffer):
+    segments of 2, 1 and 2 frames, downscale (BASELINE configs[3]'s 2:1 filters) and an
+    upscale, byte-equal to the oracle (swscale bicubic + encode)."""
+    import torch
+    frames = rand_frames(w, h, 5, seed=w + dh, kind="smooth")
+    segs = [torch.from_numpy(frames[a:b].copy()).to("cuda:0") for a, b in ((0, 2), (2, 3), (3, 5))]
+    torch.cuda.synchronize()
+    with MjpegEncoder(0, w, h, dw, dh, qscale=q, max_batch=5) as enc:
+        enc.submit_segments([(t.data_ptr(), t.shape[0]) for t in segs])
+        enc.sync()
+        got = enc.fetch()
+    ref = oracle_frames(frames, w, h, q, False, dw, dh)
+    for i in range(5):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
 def test_submit_segments_rejects_bad_lists():
     """Errors, not undefined behaviour: no segments, more than mjg_max_segments(), a total
-    over max_batch, an empty segment, and a -vf scale profile."""
+    over max_batch, an empty segment, and the opt-in fused scale kernel."""
     import torch
     from ffmpeg_distributed_amd._lib import MjgError
     w, h = 64, 48
@@ -435,9 +453,10 @@ def test_submit_segments_rejects_bad_lists():
                 enc.submit_segments(bad)
         enc.submit_segments([(t.data_ptr(), 2), (t.data_ptr(), 2)])  # still usable
         assert len(enc.sync()) == 4
-    with MjpegEncoder(0, w, h, 32, 24, qscale=5, max_batch=4) as enc:
+    big = torch.zeros((1, i420_frame_bytes(1280, 720)), dtype=torch.uint8, device="cuda:0")
+    with MjpegEncoder(0, 1280, 720, 640, 360, qscale=5, max_batch=1, fused=True) as enc:  # fusable
         with pytest.raises(MjgError):
-            enc.submit_segments([(t.data_ptr(), 1)])
+            enc.submit_segments([(big.data_ptr(), 1)])
 
 
 def test_8k_yuvj420p_matches_oracle():
