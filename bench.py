@@ -148,7 +148,7 @@ def segments_per_launch(a, pool, seg, nseg_pool, W, H, DW, DH, FULL, Q, HUFF, de
         if k > nseg_pool:
             continue
         enc = MjpegEncoder(device, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=k * seg,
-                           huffman=HUFF)
+                           huffman=HUFF, merge=False)
         if k > enc.max_segments:
             enc.close()
             continue
@@ -157,7 +157,7 @@ def segments_per_launch(a, pool, seg, nseg_pool, W, H, DW, DH, FULL, Q, HUFF, de
         def run(n, s0):
             for s in range(s0, s0 + n):
                 enc.submit_segments([(ptrs[(s * k + i) % nseg_pool], seg) for i in range(k)])
-                if enc.pending == enc.depth:
+                if enc.pending == enc.host_depth:
                     enc.sync()
             while enc.pending:
                 enc.sync()
@@ -235,6 +235,23 @@ E2E_ARGS = {  # remote_args of each workload (fd.py:190 splits them from the CLI
 }
 
 
+def parse_worker_trace(line: str) -> dict:
+    """worker.py's `mjg-trace: frames=N total=S setup=S read=S ...` line: the float phases
+    (seconds) and the placement text after them."""
+    out, rest = {}, []
+    for tok in line.split()[1:]:
+        k, sep, v = tok.partition("=")
+        if k in ("frames", "total", "setup", "read", "submit", "sync", "fetch", "mux", "wait"):
+            try:
+                out[k] = float(v)
+                continue
+            except ValueError:
+                pass
+        rest.append(tok)
+    out["placement"] = " ".join(rest)
+    return out
+
+
 def e2e(workload: str, device: int, segments: int, tmpdir=None):
     """End-to-end frames/s through the reference's worker contract (fd.py:131-141: segment
     file on stdin, Matroska on stdout, progress on stderr, exit code), timed outside the
@@ -268,8 +285,11 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
         out["segment_bytes"] = nbytes
         out["segment_write_s"] = round(time.monotonic() - t, 2)
 
+        traces = []
+
         def leg(run_one, n):
             secs = []
+            traces.clear()
             for i in range(n):
                 dst = os.path.join(d, f"out{i % 2}.mkv")
                 t0 = time.monotonic()
@@ -278,19 +298,29 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
                 if rc != 0:
                     raise RuntimeError(f"segment {i} exited {rc}")
             steady = statistics.median(secs[1:]) if n > 1 else secs[0]
-            return {"segments": n, "first_segment_s": round(secs[0], 4),
-                    "steady_s_per_segment": round(steady, 4), "fps_steady": round(seg_frames / steady, 1),
-                    "seconds": [round(x, 4) for x in secs]}
+            r = {"segments": n, "first_segment_s": round(secs[0], 4),
+                 "steady_s_per_segment": round(steady, 4), "fps_steady": round(seg_frames / steady, 1),
+                 "seconds": [round(x, 4) for x in secs]}
+            if len(traces) > 1:  # the worker's MJG_WORKER_TRACE phases, median over the steady segments
+                keys = [k for k in traces[-1] if isinstance(traces[-1][k], float)]
+                r["worker_trace_median_s"] = {k: round(statistics.median(t[k] for t in traces[1:] if k in t), 4)
+                                              for k in keys}
+                r["worker_trace_placement"] = traces[-1].get("placement")
+            return r
 
         def per_process(resident):
             argv = D.worker_argv(host, args, resident=resident)
+            env = dict(os.environ, MJG_WORKER_TRACE="1")  # one mjg-trace: line per segment (worker.py)
 
             def one(dst):
                 with open(seg, "rb") as fi, open(dst, "wb") as fo:
-                    p = D.FFMPEGProc(argv, stdin=fi, stdout=fo)
+                    p = D.FFMPEGProc(argv, stdin=fi, stdout=fo, env=env)
                     rc = p.run()
                 if rc != 0:
                     sys.stderr.write(p.stderr[-2000:])
+                for line in p.stderr.splitlines():
+                    if line.startswith("mjg-trace:"):
+                        traces.append(parse_worker_trace(line))
                 return rc
             return one
 
@@ -339,14 +369,18 @@ def load_pmc(workload, content, digest):
     if d.get("library_digest") != digest:
         return {}, (f"{os.path.relpath(path, ROOT)} was counted on library {str(d.get('library_digest'))[:12]}, "
                     f"this run loaded {digest[:12]}: traffic not reported")
-    return d.get("kernels", {}), os.path.relpath(path, ROOT)
+    fpl = d.get("workload", {}).get("frames_per_launch") or WORKLOADS[workload][5]
+    # per frame: the PMC passes count single-segment launches (tools/pmc_workload.py syncs each),
+    # the bench's launches may carry two merged segments
+    kern = {k: dict(v, hbm_bytes_per_frame=v["hbm_bytes_per_launch"] / fpl) for k, v in d.get("kernels", {}).items()}
+    return kern, os.path.relpath(path, ROOT)
 
 
-def pmc_traffic(pmc, *names):
-    """HBM bytes per launch of the kernels whose names contain any of `names` (None when the
-    PMC file has none of them)."""
-    hit = [v["hbm_bytes_per_launch"] for k, v in pmc.items() if any(n in k for n in names)]
-    return sum(hit) if hit else None
+def pmc_traffic(pmc, fpl, *names):
+    """HBM bytes per launch of `fpl` frames of the kernels whose names contain any of `names`
+    (None when the PMC file has none of them)."""
+    hit = [v["hbm_bytes_per_frame"] * fpl for k, v in pmc.items() if any(n in k for n in names)]
+    return round(sum(hit)) if hit else None
 
 
 def roofline_entry(kernel, alg_bytes, ms, traffic, what):
@@ -356,45 +390,49 @@ def roofline_entry(kernel, alg_bytes, ms, traffic, what):
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4), "bytes": what}
 
 
-def rooflines(kt, seg, mean_jpeg, pmc, optimal, scaled, step_ms=None):
-    """Per-kernel roofline entries (SURVEY §8d bytes) and the primary one (reads the input).
-    step_ms: the submits of consecutive segments run on two streams and their launches overlap
-    (csrc/api.hip alloc_slot: the next launch starts in the previous one's drain), so a kernel's
-    event interval includes time shared with the other submit's kernels; the primary entry is
-    then the bytes of one step over the wall time per step (the per-kernel entries stay as
-    measured, overlap included)."""
-    src_b, dst_b, jpeg_b = frame_bytes(W, H) * seg, frame_bytes(DW, DH) * seg, mean_jpeg * seg
+def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
+    """Per-kernel roofline entries (SURVEY §8d bytes per launch: `fpl` frames per launch, a
+    merged launch carrying two segments) and the primary one (reads the input).
+    step_ms: consecutive launches run on two streams and overlap (csrc/api.hip alloc_slot: the
+    next launch starts in the previous one's drain), so a kernel's event interval includes time
+    shared with the other launch's kernels; the primary entry is then one step's bytes (`seg`
+    frames) over the wall time per step, which the kernel trace's launch period reproduces
+    (tools/timeline.py, profiles/r05*_timeline.txt); the per-kernel entries stay as measured,
+    overlap included, and bench.py adds isolated launches beside them."""
+    src_b, dst_b, jpeg_b = frame_bytes(W, H) * fpl, frame_bytes(DW, DH) * fpl, mean_jpeg * fpl
+    sstep = (seg or fpl) / fpl  # one step's share of a launch's bytes
     out = []
     if scaled and kt.get("scale", 0) > 0:  # unfused: k_scale writes the scaled planes to HBM
-        out.append(roofline_entry("k_scale", src_b + dst_b, kt["scale"], pmc_traffic(pmc, "k_scale"),
+        out.append(roofline_entry("k_scale", src_b + dst_b, kt["scale"], pmc_traffic(pmc, fpl, "k_scale"),
                                   "source planes read + scaled planes written"))
         enc_in = dst_b
     else:
         enc_in = src_b
     if optimal:
         out.append(roofline_entry("k_encode<count> + k_huff_build", enc_in, kt["huff"],
-                                  pmc_traffic(pmc, "k_encode", "k_huff_build"),
+                                  pmc_traffic(pmc, fpl, "k_encode", "k_huff_build"),
                                   "input planes read (symbol records are not credited)"))
-        out.append(roofline_entry("k_emit_syms", jpeg_b, kt["encode"], pmc_traffic(pmc, "k_emit_syms"),
+        out.append(roofline_entry("k_emit_syms", jpeg_b, kt["encode"], pmc_traffic(pmc, fpl, "k_emit_syms"),
                                   "JPEG scan bits written"))
         primary = roofline_entry("count pass + emission (k_encode<count>, k_huff_build, k_emit_syms)"
                                  + (", wall time per step" if step_ms else ""),
-                                 enc_in + jpeg_b, step_ms or (kt["huff"] + kt["encode"]),
-                                 pmc_traffic(pmc, "k_encode", "k_huff_build", "k_emit_syms"),
+                                 (enc_in + jpeg_b) * (sstep if step_ms else 1), step_ms or (kt["huff"] + kt["encode"]),
+                                 pmc_traffic(pmc, fpl, "k_encode", "k_huff_build", "k_emit_syms"),
                                  "input planes read + JPEG written")
     else:
         name = "k_encode" if not (scaled and kt.get("scale", 0) == 0) else "k_scale_encode (fused)"
         out.append(roofline_entry(name, enc_in + jpeg_b, kt["encode"],
-                                  pmc_traffic(pmc, "k_encode", "k_scale_encode"),
+                                  pmc_traffic(pmc, fpl, "k_encode", "k_scale_encode"),
                                   ("scaled" if enc_in == dst_b and scaled else "input") +
                                   " planes read + JPEG written"))
         primary = out[0]
         if scaled and step_ms:
-            primary = roofline_entry("k_scale + k_encode, wall time per step", src_b + jpeg_b, step_ms,
+            primary = roofline_entry("k_scale + k_encode, wall time per step", (src_b + jpeg_b) * sstep, step_ms,
                                      None, "source planes read + JPEG written")
         elif step_ms:
-            primary = roofline_entry(name + ", wall time per step (launches overlap)", enc_in + jpeg_b, step_ms,
-                                     out[0]["traffic"], out[0]["bytes"])
+            tr = out[0]["traffic"]
+            primary = roofline_entry(name + ", wall time per step (launches overlap)", (enc_in + jpeg_b) * sstep,
+                                     step_ms, None if tr is None else round(tr * sstep), out[0]["bytes"])
     return primary, out
 
 
@@ -472,12 +510,20 @@ def main():
             bytes_out.append(int(enc.sync().sum()))
         torch.cuda.synchronize()
 
+    def trace_marker():
+        # a tiny kernel on torch's stream (rocprofv3 kernel trace: "spin_kernel"), outside the
+        # timed region, that brackets the timed steps' launches for tools/timeline.py
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
+
     def reset():
         drain_and_sync()
         enc.kernel_times(reset=True)
         bytes_out.clear()
+        trace_marker()
 
     dt = timed_region(step, a.warmup, a.steps, barrier, drain_and_sync, reset)
+    trace_marker()
     if a.no_kernel_timing:
         from ffmpeg_distributed_amd._lib import KERNEL_NAMES
         kt, nl = {k: 0.0 for k in KERNEL_NAMES}, 0
@@ -488,13 +534,45 @@ def main():
     frames_total = a.steps * seg * world
     value = frames_total / dt
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
+    fpl = a.steps * seg / nl if nl else seg  # frames per launch (merged launches carry two segments)
     pmc, pmc_src = (load_pmc(a.workload, a.content, B.source_digest())
                     if (seg == SEG and not a.rst and not a.fused and a.dct == "auto"
                         and HUFF == WORKLOADS[a.workload][7]) else ({}, "no PMC pass for this configuration"))
-    overlap = True  # consecutive submits run on two streams (csrc/api.hip alloc_slot; see rooflines)
-    primary, per_kernel = rooflines(kt, seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H),
-                                    dt / a.steps * 1e3 if overlap else None)
-    primary = dict(primary, launches=nl, traffic_source=pmc_src)
+    overlap = True  # consecutive launches run on two streams (csrc/api.hip alloc_slot; see rooflines)
+    primary, per_kernel = rooflines(kt, fpl, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H),
+                                    dt / a.steps * 1e3 if overlap else None, seg)
+    primary = dict(primary, launches=nl, frames_per_launch=round(fpl, 2), traffic_source=pmc_src)
+
+    # isolated launches (after the timed region, each synced before the next, so nothing
+    # overlaps them): the kernels' own duration, one segment per launch (the main context: a
+    # submit to an idle GPU launches at once) and two segments per launch (the shape of a
+    # merged launch, as one two-segment list on a context of twice the frames)
+    iso = []
+    if not a.no_kernel_timing and not a.fused:
+        for k in (1, 2):
+            if k > nseg_pool:
+                continue
+            e2 = enc if k == 1 else MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=k * seg,
+                                                  timing=True, huffman=HUFF, rst=a.rst, merge=False,
+                                                  dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
+            e2.kernel_times(reset=True)
+            for r in range(4):
+                segs = [(pool[((r * k + i) % nseg_pool) * seg].data_ptr(), seg) for i in range(k)]
+                if k == 1:
+                    e2.submit(device_ptr=segs[0][0], nframes=seg)
+                else:
+                    e2.submit_segments(segs)
+                e2.sync()
+            kti, nli = e2.kernel_times(reset=True)
+            if e2 is not enc:
+                e2.close()
+            _, ents = rooflines(kti, k * seg, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H))
+            for e in ents:
+                e["kernel"] += f" (isolated: {k} segment{'s' if k > 1 else ''} per launch, synced)"
+                e["launches"] = nli
+            iso += ents
+        per_kernel += iso
+        trace_marker()
 
     batched = None
     if a.segments_per_launch and world == 1 and not a.fused and not a.rst and nseg_pool >= 2:

@@ -30,6 +30,7 @@ MJG_F_TIMING_DETAIL = 64
 MJG_F_FUSED = 128
 MJG_F_DCT_MFMA = 256
 MJG_F_DCT_VALU = 512
+MJG_F_NO_MERGE = 1024
 
 # mjg_config.chroma_format
 CHROMA_FORMATS = {"420": 0, "422": 1, "444": 2}
@@ -41,7 +42,7 @@ MJG_NUM_KERNELS = len(KERNEL_NAMES)
 EXPORTS = (
     "mjg_version", "mjg_last_error", "mjg_device_count", "mjg_device_numa_node", "mjg_open", "mjg_close",
     "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch", "mjg_fetch_host",
-    "mjg_output_device", "mjg_stream", "mjg_queue_depth", "mjg_submit_segments", "mjg_max_segments", "mjg_host_alloc", "mjg_host_free",
+    "mjg_output_device", "mjg_stream", "mjg_queue_depth", "mjg_ctx_queue_depth", "mjg_submit_segments", "mjg_max_segments", "mjg_host_alloc", "mjg_host_free",
     "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
     "mjg_debug_planes", "mjg_debug_filter",
 )
@@ -99,6 +100,9 @@ def load():
         if hasattr(L, "mjg_queue_depth"):  # absent from libraries built before r04 (A/B builds)
             L.mjg_queue_depth.argtypes = []
             L.mjg_queue_depth.restype = C.c_int
+        if hasattr(L, "mjg_ctx_queue_depth"):  # absent from libraries built before r05 (A/B builds)
+            L.mjg_ctx_queue_depth.argtypes = [vp]
+            L.mjg_ctx_queue_depth.restype = C.c_int
         if hasattr(L, "mjg_submit_segments"):  # absent from libraries built before r04 (A/B builds)
             L.mjg_submit_segments.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_int), C.c_int]
             L.mjg_max_segments.argtypes = []
@@ -113,10 +117,10 @@ def load():
         L.mjg_build_header.argtypes = [C.POINTER(MjgConfig), u8p, sz, C.POINTER(sz)]
         L.mjg_sws_filter.argtypes = [C.c_int] * 7 + [C.POINTER(C.c_int16), sz, C.POINTER(C.c_int32),
                                                      C.POINTER(C.c_int)]
-        # fail loudly on a stale / partial build (an A/B library from before r04 named by
-        # MJG_LIBRARY may lack mjg_queue_depth: the queue is then two deep; and the
-        # multi-segment submit, which only bench.py's segments_per_launch leg calls)
-        late = (("mjg_queue_depth", "mjg_submit_segments", "mjg_max_segments")
+        # fail loudly on a stale / partial build (an A/B library from before r04/r05 named by
+        # MJG_LIBRARY may lack mjg_queue_depth / mjg_ctx_queue_depth: the queue is then two
+        # deep, no merging; and the multi-segment submit, which encoder.submit_segments guards)
+        late = (("mjg_queue_depth", "mjg_ctx_queue_depth", "mjg_submit_segments", "mjg_max_segments")
                 if os.environ.get("MJG_LIBRARY") else ())
         for name in EXPORTS:
             if name not in late:

@@ -178,14 +178,23 @@ struct PlaneScale {
 // workgroups dispatch before the next k_encode's).  Three slots measured 10% slower: three
 // k_encode launches then share the CUs (DESIGN §4 streams; tools/patches.py slots3).
 constexpr int kSlots = 2;
+// Library-side merging (r05): single-segment device submits are held while the GPU has a
+// launch queued and launched kMerge at a time as one segment list (submit_impl's SegList),
+// so the launch's ramp and drain (T(n) = 0.115 ms + 4.48 us n per 4K launch) is
+// paid once per kMerge submits.  Each submit stays a job of its own for mjg_sync / mjg_fetch.
+constexpr int kMerge = 2;
+// merging is off when the slots' doubled scratch would take more than this share of the
+// device's free memory (slot buffers scale with the frames a launch may carry)
+constexpr double kMergeMemShare = 0.25;
 struct Slot {
   bool alloc = false, pending = false;
+  int njobs = 0, nsynced = 0;       // submits (jobs) this launch carries / already synced
+  int jf0[kMaxSegs] = {}, jn[kMaxSegs] = {};  // each job's first frame in the launch, frames
   hipStream_t st = nullptr;        // H2D, scale and k_encode of this slot's submits
   uint8_t *d_stage = nullptr;      // H2D staging for host submits (allocated on first use)
   uint8_t *d_scaled = nullptr;     // -vf scale: k_scale's output planes
   uint32_t *d_stage_bits = nullptr;  // k_encode: per wave, lane-major staging of blocks past 128 bits
-  int n = 0;
-  uint64_t total = 0;
+  int n = 0;  // frames of the launch
   uint32_t *d_scratch = nullptr;
   uint32_t *d_stream = nullptr;  // k_count_ff's realigned words, per segment (k_write reads them)
   uint32_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_group_ff = nullptr, *d_ff_off = nullptr;
@@ -239,10 +248,17 @@ struct mjg_ctx {
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
 
   Slot slot[kSlots];
-  int head = 0;   // slot of the next submit
-  int nout = 0;   // submits queued and not synced (0..kSlots)
-  int last = -1;  // slot of the last synced submit (fetch / output_device / debug read it)
+  int head = 0;   // slot of the next launch
+  int nout = 0;   // launches with jobs not yet synced (0..kSlots)
+  int last = -1;  // slot of the last synced job (fetch / output_device / debug read it)
+  int last_job = 0;            // that job's index in its launch
+  uint64_t last_off = 0, last_total = 0;  // its packed bytes' offset in the launch's d_out, size
   bool synced_since_submit = false;
+  int merge = 1;               // jobs per launch for single-segment device submits (kMerge or 1)
+  int held = 0;                // device jobs held for the next launch (0..merge)
+  const uint8_t *held_p[kMaxSegs] = {};
+  int held_n[kMaxSegs] = {};
+  int launches = 0;            // launches since open (tests / diagnostics)
 
   bool timing = false, timing_detail = false;
   uint8_t *h_fetch = nullptr;  // page-locked copy of the last fetched output (mjg_fetch_host)
@@ -716,7 +732,21 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     }
   }
 
-  const size_t B = (size_t)k.max_batch, NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
+  const size_t NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
+  // merging (kMerge): not with the opt-in fused kernel (no segment lists) or MJG_F_NO_MERGE;
+  // MJG_MERGE=1 turns it off for a process (A/B), =2..4 sets the jobs per launch
+  c->merge = kMerge;
+  if (const char *e = getenv("MJG_MERGE")) c->merge = std::max(1, std::min(kMaxSegs, atoi(e)));
+  if ((k.flags & MJG_F_NO_MERGE) || (k.flags & MJG_F_FUSED)) c->merge = 1;
+  if (c->merge > 1) {  // slot buffers for merge * max_batch frames: within a share of free memory
+    size_t fr = 0, tot = 0;
+    HIP_TRY(hipMemGetInfo(&fr, &tot));
+    const double per_frame = 2.0 * (double)NC * kSlotWords * 4 + 2.0 * (double)c->enc_frame_bytes;
+    if (kSlots * (double)c->merge * (double)k.max_batch * per_frame > kMergeMemShare * (double)fr) c->merge = 1;
+  }
+  if ((unsigned long long)k.max_batch * c->merge * g.nseg * g.nchunks * g.nchunks >= ((unsigned long long)1 << 40))
+    c->merge = 1;  // merged launches would overflow k_encode's task magic (checked for max_batch above)
+  const size_t B = (size_t)k.max_batch * (size_t)c->merge;  // frames one launch may carry
   int rc;
   if ((rc = dmalloc(&c->d_tabs, kTabWords)) || (rc = dmalloc(&c->d_hdr, c->hdr.size()))) return rc;
   c->slot_B = B;
@@ -950,7 +980,7 @@ namespace {
 // mjg_submit's body; segs (mjg_submit_segments: device frames, no -vf scale) replaces the one
 // segment at `frames` as k_encode's input
 int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, const SegList *segs) {
-  if (n < 1 || n > c->cfg.max_batch)
+  if (n < 1 || (size_t)n > c->slot_B || (!src_is_device && n > c->cfg.max_batch))
     return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
   if (c->nout == kSlots) return set_err(MJG_E_STATE, "%d submits queued: sync one first", kSlots);
   HIP_TRY(hipSetDevice(c->device));
@@ -1088,7 +1118,7 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
   HIP_TRY(hipGetLastError());
   // segment and frame sizes, the frames' packed offsets
   tmark(c, S, MJG_K_SCAN_FF, 0);
-  k_scan_ff<<<n, 256, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, gps, g.nseg, (int)c->hdr.size(),
+  k_scan_ff<<<n, 256, 0, c->tail>>>(S.d_group_ff, S.d_ff_off, S.d_frame_bits, g.nchunks, gps, g.nseg, (int)c->hdr.size(),
                                       c->optimal ? S.d_dht_nval : nullptr, S.d_hdr_lens, S.d_seg_size,
                                       S.d_seg_off, S.d_frame_size, S.d_frame_offsets, S.d_done);
   tmark(c, S, MJG_K_SCAN_FF, 1);
@@ -1097,15 +1127,84 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
   if (rc) return rc;
   S.n = n;
   S.pending = true;
+  S.njobs = 1;  // the caller records a merged launch's jobs
+  S.nsynced = 0;
+  S.jf0[0] = 0;
+  S.jn[0] = n;
   c->head = (c->head + 1) % kSlots;
   c->nout++;
+  c->launches++;
   c->synced_since_submit = false;
   return MJG_OK;
+}
+
+// Jobs submitted and not yet synced: those of the queued launches plus the held ones.
+int pending_jobs(const mjg_ctx *c) {
+  int p = c->held;
+  for (int i = 0; i < c->nout; i++) {
+    const Slot &S = c->slot[(c->head + kSlots - c->nout + i) % kSlots];
+    p += S.njobs - S.nsynced;
+  }
+  return p;
+}
+
+// One launch for the held device jobs: their frames as a segment list (one job: the plain
+// single-segment launch), each job's frames recorded for mjg_sync.
+int launch_held(mjg_ctx *c) {
+  SegList sl;
+  int n = 0;
+  for (int k = 0; k < kMaxSegs; k++) {
+    sl.p[k] = c->held_p[k < c->held ? k : 0];
+    sl.f0[k] = k < c->held ? n : INT_MAX;
+    if (k < c->held) n += c->held_n[k];
+  }
+  Slot &S = c->slot[c->head];
+  const int rc = submit_impl(c, c->held_p[0], n, 1, c->held > 1 ? &sl : nullptr);
+  if (rc) return rc;  // the jobs stay held
+  S.njobs = c->held;
+  for (int k = 0, f = 0; k < c->held; f += c->held_n[k], k++) {
+    S.jf0[k] = f;
+    S.jn[k] = c->held_n[k];
+  }
+  c->held = 0;
+  return MJG_OK;
+}
+
+// Launch the held jobs when a launch slot is free and either they are `merge` jobs or the GPU
+// has nothing else queued (a lone job is never held back from an idle GPU).  At mjg_sync the
+// slot of the job just synced stays untouched: its results are read (mjg_fetch,
+// mjg_output_device) until the caller's next submit.
+int try_launch_held(mjg_ctx *c, bool at_sync) {
+  if (!c->held || c->nout == kSlots) return MJG_OK;
+  if (c->held < c->merge && c->nout > 0) return MJG_OK;
+  if (at_sync && c->head == c->last) return MJG_OK;
+  return launch_held(c);
 }
 }  // namespace
 
 int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (!c || !frames) return set_err(MJG_E_INVALID, "null argument");
+  if (n < 1 || n > c->cfg.max_batch)
+    return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
+  if (src_is_device && c->merge > 1) {  // held, and launched with the next one(s)
+    if (pending_jobs(c) >= kSlots * c->merge || c->held == c->merge)
+      return set_err(MJG_E_STATE, "%d submits queued: sync one first", pending_jobs(c));
+    c->held_p[c->held] = frames;
+    c->held_n[c->held] = n;
+    c->held++;
+    c->synced_since_submit = false;
+    const int rc = try_launch_held(c, false);
+    if (rc) c->held--;
+    return rc;
+  }
+  // host frames (H2D through the slot's staging) or merging off: a launch of its own, after
+  // a launch of the jobs held before it
+  if (c->nout + (c->held ? 1 : 0) >= kSlots)
+    return set_err(MJG_E_STATE, "%d launches queued: sync one first", kSlots);
+  if (c->held) {
+    const int rc = launch_held(c);
+    if (rc) return rc;
+  }
   return submit_impl(c, frames, n, src_is_device, nullptr);
 }
 
@@ -1129,51 +1228,77 @@ int mjg_submit_segments(mjg_ctx *c, const uint8_t *const *seg_frames, const int 
       sl.f0[k] = INT_MAX;
     }
   }
+  if (n > c->cfg.max_batch) return set_err(MJG_E_INVALID, "%d frames in the segments, max_batch %d", n, c->cfg.max_batch);
+  if (c->nout + (c->held ? 1 : 0) >= kSlots)
+    return set_err(MJG_E_STATE, "%d launches queued: sync one first", kSlots);
+  if (c->held) {
+    const int rc = launch_held(c);
+    if (rc) return rc;
+  }
   return submit_impl(c, seg_frames[0], n, 1, &sl);
 }
 
-// Completes the oldest queued submit (or, with none queued, reports the last synced one).
+int mjg_ctx_queue_depth(const mjg_ctx *c) { return c ? kSlots * c->merge : 0; }
+
+// Completes the oldest queued job (or, with none queued, reports the last synced one).  The
+// first job of a launch waits for it (and regrows its output on overflow); the others of the
+// same launch are then ready.
 int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
   if (!c) return set_err(MJG_E_INVALID, "null ctx");
-  if (c->nout == 0 && c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
+  if (c->nout == 0 && c->held == 0 && c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
   HIP_TRY(hipSetDevice(c->device));
+  if (c->nout == 0 && c->held) {  // the oldest job is held: launch it now
+    const int rc = launch_held(c);
+    if (rc) return rc;
+  }
   if (c->nout > 0) {
-    const int si = (c->head + kSlots - c->nout) % kSlots;  // oldest queued submit
+    const int si = (c->head + kSlots - c->nout) % kSlots;  // oldest queued launch
     Slot &S = c->slot[si];
-    HIP_TRY(hipEventSynchronize(S.done));
-    const int n = S.n;
-    uint64_t t = 0;
-    for (int i = 0; i < n; i++) t += S.h_sizes[i];
-    if (*S.h_status & 1u) {  // packed output overflowed: grow, re-run the write pass only
-      HIP_TRY(hipFree(S.d_out));
-      S.d_out = nullptr;
-      S.out_cap = t + t / 4 + 4096;
-      int rc = dmalloc(&S.d_out, S.out_cap);
-      if (rc) return rc;
-      if ((rc = launch_write(c, S, n, true))) return rc;
+    if (S.nsynced == 0) {
       HIP_TRY(hipEventSynchronize(S.done));
-      if (*S.h_status & 1u) return set_err(MJG_E_HIP, "output overflow persisted");
-    }
-    if (c->timing) {
-      for (int k = 0; k < MJG_NUM_KERNELS; k++) {
-        if (k == MJG_K_SCALE && (!c->scale || c->fused)) continue;
-        if (k == MJG_K_HUFF && !c->optimal) continue;
-        const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
-        if (tail != c->timing_detail && (tail || k == MJG_K_TAIL)) continue;
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, S.ev[k][0], S.ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
+      const int n = S.n;
+      uint64_t t = 0;
+      for (int i = 0; i < n; i++) t += S.h_sizes[i];
+      if (*S.h_status & 1u) {  // packed output overflowed: grow, re-run the write pass only
+        HIP_TRY(hipFree(S.d_out));
+        S.d_out = nullptr;
+        S.out_cap = t + t / 4 + 4096;
+        int rc = dmalloc(&S.d_out, S.out_cap);
+        if (rc) return rc;
+        if ((rc = launch_write(c, S, n, true))) return rc;
+        HIP_TRY(hipEventSynchronize(S.done));
+        if (*S.h_status & 1u) return set_err(MJG_E_HIP, "output overflow persisted");
       }
-      c->t_n++;
+      if (c->timing) {
+        for (int k = 0; k < MJG_NUM_KERNELS; k++) {
+          if (k == MJG_K_SCALE && (!c->scale || c->fused)) continue;
+          if (k == MJG_K_HUFF && !c->optimal) continue;
+          const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
+          if (tail != c->timing_detail && (tail || k == MJG_K_TAIL)) continue;
+          float ms = 0.f;
+          if (hipEventElapsedTime(&ms, S.ev[k][0], S.ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
+        }
+        c->t_n++;
+      }
     }
-    S.total = t;
-    S.pending = false;
-    c->nout--;
+    const int j = S.nsynced;
+    uint64_t off = 0, t = 0;
+    for (int i = 0; i < S.jf0[j]; i++) off += S.h_sizes[i];
+    for (int i = S.jf0[j]; i < S.jf0[j] + S.jn[j]; i++) t += S.h_sizes[i];
+    if (++S.nsynced == S.njobs) {
+      S.pending = false;
+      c->nout--;
+    }
     c->last = si;
+    c->last_job = j;
+    c->last_off = off;
+    c->last_total = t;
+    (void)try_launch_held(c, true);  // a failed launch leaves the jobs held: their own sync reports it
   }
   c->synced_since_submit = true;
   const Slot &L = c->slot[c->last];
-  if (frame_sizes) memcpy(frame_sizes, L.h_sizes, L.n * sizeof(uint64_t));
-  if (total) *total = L.total;
+  if (frame_sizes) memcpy(frame_sizes, L.h_sizes + L.jf0[c->last_job], L.jn[c->last_job] * sizeof(uint64_t));
+  if (total) *total = c->last_total;
   return MJG_OK;
 }
 
@@ -1184,18 +1309,19 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
 // 0.1 s per 1080p segment in some worker processes and 2 ms in others.
 int mjg_fetch_host(mjg_ctx *c, const uint8_t **data, size_t *len) {
   if (!c || !data) return set_err(MJG_E_INVALID, "null argument");
-  if (c->nout > 0 && !c->synced_since_submit) {
+  if (pending_jobs(c) > 0 && !c->synced_since_submit) {
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;
   }
   if (c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
   const Slot &L = c->slot[c->last];
+  const uint64_t total = c->last_total;
   HIP_TRY(hipSetDevice(c->device));
-  if (L.total > c->h_fetch_cap) {
+  if (total > c->h_fetch_cap) {
     if (c->h_fetch) HIP_TRY(hipHostFree(c->h_fetch));
     c->h_fetch = nullptr;
     c->h_fetch_cap = 0;
-    const size_t cap = L.total + L.total / 4 + 4096;
+    const size_t cap = total + total / 4 + 4096;
     if (hipHostMalloc((void **)&c->h_fetch, cap, hipHostMallocDefault) != hipSuccess) {
       c->h_fetch = nullptr;
       (void)hipGetLastError();
@@ -1203,22 +1329,21 @@ int mjg_fetch_host(mjg_ctx *c, const uint8_t **data, size_t *len) {
     }
     c->h_fetch_cap = cap;
   }
-  if (L.total) HIP_TRY(hipMemcpy(c->h_fetch, L.d_out, L.total, hipMemcpyDeviceToHost));
+  if (total) HIP_TRY(hipMemcpy(c->h_fetch, L.d_out + c->last_off, total, hipMemcpyDeviceToHost));
   *data = c->h_fetch;
-  if (len) *len = L.total;
+  if (len) *len = total;
   return MJG_OK;
 }
 
 // mjg_fetch_host, then a copy into the caller's memory.
 int mjg_fetch(mjg_ctx *c, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  if (c->nout > 0 && !c->synced_since_submit) {
+  if (pending_jobs(c) > 0 && !c->synced_since_submit) {
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;
   }
   if (c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
-  const Slot &L = c->slot[c->last];
-  if (cap < L.total) return set_err(MJG_E_CAPACITY, "fetch needs %llu bytes", (unsigned long long)L.total);
+  if (cap < c->last_total) return set_err(MJG_E_CAPACITY, "fetch needs %llu bytes", (unsigned long long)c->last_total);
   const uint8_t *p = nullptr;
   size_t n = 0;
   const int rc = mjg_fetch_host(c, &p, &n);
@@ -1227,11 +1352,13 @@ int mjg_fetch(mjg_ctx *c, uint8_t *out, size_t cap) {
   return MJG_OK;
 }
 
+// The launch's packed output and the job's frame offsets into it (data + offsets[i] is the
+// job's frame i; with merged launches offsets[0] is the job's place in the launch's output).
 int mjg_output_device(mjg_ctx *c, const uint8_t **data, const uint64_t **offsets) {
   if (!c) return set_err(MJG_E_INVALID, "null ctx");
   const Slot &L = c->slot[c->last < 0 ? 0 : c->last];
   if (data) *data = L.d_out;
-  if (offsets) *offsets = L.d_frame_offsets;
+  if (offsets) *offsets = L.d_frame_offsets + (c->last < 0 ? 0 : L.jf0[c->last_job]);
   return MJG_OK;
 }
 
@@ -1309,18 +1436,18 @@ int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, i
 int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
   if (!c->geom.debug_coefs) return set_err(MJG_E_STATE, "context opened without MJG_F_DEBUG_COEFS");
-  if (c->nout > 0 && !c->synced_since_submit) {
+  if (pending_jobs(c) > 0 && !c->synced_since_submit) {
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;
   }
   if (c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
   const Slot &L = c->slot[c->last];
   const size_t nb = (size_t)c->geom.nmcu * c->geom.bpm;  // dbg buffer: frame-major, coding order
-  if (frame < 0 || frame >= L.n) return set_err(MJG_E_INVALID, "frame %d", frame);
+  if (frame < 0 || frame >= L.jn[c->last_job]) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (nblocks < nb) return set_err(MJG_E_CAPACITY, "need %zu blocks", nb);
   // the kernel stores each quantised block in natural (raster) order
-  HIP_TRY(hipMemcpy(out, L.d_dbg + (size_t)frame * nb * 64, nb * 64 * sizeof(int16_t),
-                    hipMemcpyDeviceToHost));
+  const size_t f = (size_t)L.jf0[c->last_job] + (size_t)frame;
+  HIP_TRY(hipMemcpy(out, L.d_dbg + f * nb * 64, nb * 64 * sizeof(int16_t), hipMemcpyDeviceToHost));
   return MJG_OK;
 }
 
@@ -1328,15 +1455,16 @@ int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
   if (!c->scale || c->fused)
     return set_err(MJG_E_STATE, "context does not scale, or scales fused (opened with MJG_F_FUSED)");
-  if (c->nout > 0) {  // the latest synced submit's planes
+  if (pending_jobs(c) > 0) {  // the latest synced submit's planes
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;
   }
-  if (c->nout > 0 || c->last < 0) return set_err(MJG_E_STATE, "sync every queued submit first");
-  if (frame < 0 || frame >= c->slot[c->last].n) return set_err(MJG_E_INVALID, "frame %d", frame);
+  if (pending_jobs(c) > 0 || c->last < 0) return set_err(MJG_E_STATE, "sync every queued submit first");
+  const Slot &L = c->slot[c->last];
+  if (frame < 0 || frame >= L.jn[c->last_job]) return set_err(MJG_E_INVALID, "frame %d", frame);
   if (cap < c->enc_frame_bytes) return set_err(MJG_E_CAPACITY, "need %zu bytes", c->enc_frame_bytes);
-  HIP_TRY(hipMemcpy(out, c->slot[c->last].d_scaled + (size_t)frame * c->enc_frame_bytes, c->enc_frame_bytes,
-                    hipMemcpyDeviceToHost));
+  const size_t f = (size_t)L.jf0[c->last_job] + (size_t)frame;
+  HIP_TRY(hipMemcpy(out, L.d_scaled + f * c->enc_frame_bytes, c->enc_frame_bytes, hipMemcpyDeviceToHost));
   return MJG_OK;
 }
 

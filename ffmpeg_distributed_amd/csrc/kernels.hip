@@ -1697,7 +1697,10 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
 // profiles/r04ad_tail_wave_priority.txt, r04ae_tail_wave_priority_levels.txt): a heavy stream's
 // tail (2-4x the bytes) then takes that much more issue from k_encode.  So the raise is kept to
 // submits whose first segment averages under kTailLightBits per chunk (BASELINE's testsrc
-// workloads 740-1440 bits, the fractal content 2190, noise-patches 3340).
+// workloads 740-1440 bits, the fractal content 2190, noise-patches 3340).  The test reads the
+// first segment's bit count, so the scans that produce it (k_scan_bits, k_scan_bits_seg: a few
+// microseconds, before any count exists) always run at kTailPrio; k_count_ff, k_scan_ff and
+// k_write apply the test with the segment's chunk count.
 constexpr int kTailPrio = 2;
 constexpr uint32_t kTailLightBits = 1800;
 __device__ __forceinline__ void tail_priority(const uint32_t *seg_bits, int nchunks) {
@@ -1779,6 +1782,7 @@ __global__ __launch_bounds__(256) void k_scan_bits_seg(uint32_t *__restrict__ ch
                                                        uint32_t *__restrict__ status,
                                                        uint32_t *__restrict__ done, int ndone) {
   const int sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  __builtin_amdgcn_s_setprio(kTailPrio);
   if (blockIdx.x == 0 && threadIdx.x < kXcds) work_ctr[threadIdx.x * kCtrStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *status = 0;
   {  // k_count_ff's ticket counters
@@ -1990,13 +1994,13 @@ __global__ __launch_bounds__(256) void k_count_ff(const uint32_t *__restrict__ s
 // (one ticket per frame, done[0], zeroed by k_scan_bits) places every frame: frame_offsets.
 __global__ __launch_bounds__(256) void k_scan_ff(const uint32_t *__restrict__ group_ff,
                                                  uint32_t *__restrict__ ff_off,
-                                                 const uint32_t *__restrict__ seg_bits, int gps, int nseg,
+                                                 const uint32_t *__restrict__ seg_bits, int nchunks, int gps, int nseg,
                                                  int hdr_len, const uint32_t *__restrict__ dht_nval,
                                                  uint32_t *__restrict__ hdr_lens, uint32_t *__restrict__ seg_size,
                                                  uint32_t *__restrict__ seg_off, uint64_t *__restrict__ frame_size,
                                                  uint64_t *__restrict__ frame_offsets, uint32_t *__restrict__ done) {
   __shared__ uint32_t s_last;
-  tail_priority(seg_bits, gps * kChunksPerWave);
+  tail_priority(seg_bits, nchunks);
   const int f = blockIdx.x, nframes = gridDim.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t mine = 0;  // nseg == 1: the segment's size (wave 0)
   for (int si = wave; si < nseg; si += 4) {

@@ -28,12 +28,16 @@
 //   mjg_client --device N --socket-name     (prints the encoder's socket name)
 //
 // Wire format (little-endian), client -> encoder, one message with SCM_RIGHTS {0, 1, 2}:
-//   "MJG1" u32 total_bytes u32 kind (0 encode, 1 shutdown) u32 nargs u32 nenv, then nargs
+//   "MJG2" u32 total_bytes u32 kind (0 encode, 1 shutdown) u32 nargs u32 nenv, then nargs
 //   NUL-terminated arguments and nenv NUL-terminated "NAME=VALUE" strings (the MJG_* settings
 //   of this process's environment); encoder -> client: the byte 'A' once the request is read
 //   (before any of the segment is), then the i32 exit code.  A connection that ends before the
 //   'A' (an encoder closing its socket at its idle timeout while this client queued) touched
 //   nothing of the segment: the client connects again, starting an encoder if none listens.
+//   Any other first byte is a hard error (never a retry: the request may have been consumed).
+//   "MJG2" (r05): the 'A' acknowledgement; an encoder of the older "MJG1" protocol refuses the
+//   request as malformed and closes the connection before any byte, which the retry loop then
+//   meets three times and reports.
 #define _GNU_SOURCE
 #include <errno.h>
 #include <fcntl.h>
@@ -53,7 +57,7 @@
 
 extern char **environ;
 
-static const char *kMagic = "MJG1";
+static const char *kMagic = "MJG2";
 
 static int die(const char *dev, const char *msg, int err) {
   if (err)
@@ -98,6 +102,8 @@ static int sock_name(const char *dev, const char *pkg, char *name, size_t cap) {
   h = fnv(h, ml);
   h = fnv(h, getenv("MJG_NUMA_BIND"));
   h = fnv(h, getenv("MJG_SERVE_BATCH_BYTES"));
+  h = fnv(h, getenv("MJG_MERGE"));  // read once by the library at mjg_open
+  h = fnv(h, kMagic);  // the protocol: a client never meets an encoder of another wire format
   snprintf(name, cap, "mjg-gpu-%u-%s-%llx-%llx-%llx", (unsigned)getuid(), dev, (unsigned long long)st.st_ino,
            (unsigned long long)st.st_mtim.tv_sec * 1000000000ull + (unsigned long long)st.st_mtim.tv_nsec,
            (unsigned long long)h);
@@ -299,13 +305,20 @@ int main(int argc, char **argv) {
     const int rc_send = send_all_fds(sk, buf, len, !shutdown_req);
     unsigned char ack = 0;
     ssize_t k = -1;
-    if (rc_send == 0)
+    int rerr = 0;
+    if (rc_send == 0) {
       do k = read(sk, &ack, 1);
       while (k < 0 && errno == EINTR);
+      rerr = k < 0 ? errno : 0;
+    }
     if (k == 1 && ack == 'A') break;
     close(sk);
-    // no 'A': the encoder closed this connection unread (idle exit); nothing of the segment
-    // was consumed, so connect again (a few times at most)
+    if (k == 1)  // a byte that is not the acknowledgement: another protocol; never resend
+      return die(dev, "the resident encoder answered outside the MJG2 protocol", 0);
+    if (k < 0 && rerr != ECONNRESET && rerr != EPIPE)
+      return die(dev, "reading the resident encoder's acknowledgement", rerr);
+    // EOF / reset before the 'A': the encoder closed this connection unread (idle exit);
+    // nothing of the segment was consumed, so connect again (a few times at most)
     if (attempt == 3) return die(dev, "the resident encoder keeps closing the connection", rc_send < 0 ? -rc_send : 0);
     const struct timespec ts = {0, 20000000};  // 20 ms
     nanosleep(&ts, NULL);

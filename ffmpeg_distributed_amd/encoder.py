@@ -56,7 +56,7 @@ class MjpegEncoder:
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
                  debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
                  huffman: str = "default", chroma: str = "420", rst: bool = False,
-                 fused: bool = False, dct_mfma: Optional[bool] = None):
+                 fused: bool = False, dct_mfma: Optional[bool] = None, merge: bool = True):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -88,6 +88,10 @@ class MjpegEncoder:
             flags |= _lib.MJG_F_DCT_MFMA
         elif dct_mfma is False:
             flags |= _lib.MJG_F_DCT_VALU
+        # library-side merging of single-segment device submits (mjg_submit); merge=False: every
+        # submit is a launch of its own
+        if not merge:
+            flags |= _lib.MJG_F_NO_MERGE
         self.huffman = huffman
         self.chroma = str(chroma)
         if self.chroma not in _lib.CHROMA_FORMATS:
@@ -143,13 +147,24 @@ class MjpegEncoder:
 
     @property
     def depth(self) -> int:
-        """Submits the library queues before one must be synced (mjg_queue_depth)."""
+        """Device-pointer submits (submit(device_ptr=...)) pending at most before one must be
+        synced (mjg_ctx_queue_depth: two launches of up to two merged submits)."""
+        if hasattr(self._L, "mjg_ctx_queue_depth"):
+            return int(self._L.mjg_ctx_queue_depth(self._h))
+        return self.host_depth
+
+    @property
+    def host_depth(self) -> int:
+        """Host-buffer submits and submit_segments() calls pending at most before one must be
+        synced: each takes a launch of its own (mjg_queue_depth)."""
         return int(self._L.mjg_queue_depth()) if hasattr(self._L, "mjg_queue_depth") else 2
 
     def submit(self, frames=None, nframes: Optional[int] = None, device_ptr: Optional[int] = None):
         """Queue `nframes` packed frames: a host buffer (numpy / bytes) or a device pointer
-        (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU).  Up to `depth` submits may be
-        queued; each one's k_encode runs beside the previous one's drain and tail kernels."""
+        (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU, kept alive until its sync).
+        Up to `host_depth` host submits may be queued (each one's k_encode runs beside the
+        previous one's drain and tail kernels), up to `depth` device submits: the library
+        holds a device submit while a launch is queued and launches it with the next one."""
         if device_ptr is not None:
             if nframes is None:
                 raise ValueError("nframes is required with device_ptr")
@@ -173,7 +188,10 @@ class MjpegEncoder:
         (device_ptr, nframes) on this GPU, at most mjg_max_segments() of them, totalling at
         most max_batch frames; not with fused=True.  One launch per kernel covers them
         all; sync() then returns the frames' sizes in segment order and fetch() their JPEGs,
-        the same bytes as one submit() per segment."""
+        the same bytes as one submit() per segment.  Every segment's device buffer must stay
+        alive until this submit is synced (the kernels read it in place)."""
+        if not hasattr(self._L, "mjg_submit_segments"):
+            raise MjgError(_lib.MJG_E_STATE, "library lacks mjg_submit_segments")
         k = len(segments)
         ptrs = (C.c_void_p * max(k, 1))(*[C.c_void_p(int(p)) for p, _ in segments])
         ns = (C.c_int * max(k, 1))(*[int(n) for _, n in segments])
@@ -184,6 +202,8 @@ class MjpegEncoder:
     @property
     def max_segments(self) -> int:
         """Most segments one submit_segments() may carry (mjg_max_segments)."""
+        if not hasattr(self._L, "mjg_max_segments"):
+            raise MjgError(_lib.MJG_E_STATE, "library lacks mjg_max_segments")
         return int(self._L.mjg_max_segments())
 
     def sync(self) -> np.ndarray:

@@ -37,7 +37,7 @@ from typing import Dict, List, Tuple
 
 from . import worker
 
-MAGIC = b"MJG1"
+MAGIC = b"MJG2"                      # r05: the ACK byte is part of the protocol (mjg_client.c)
 KIND_ENCODE, KIND_SHUTDOWN = 0, 1
 HEADER = struct.Struct("<4sIIII")   # magic, total bytes, kind, nargs, nenv
 MAX_REQUEST = 1 << 20

@@ -549,7 +549,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
                 raise item
             i, n = item
             if n:
-                if len(queued) == 2:
+                if len(queued) == enc.host_depth:  # host submits: one launch each
                     drain_one()
                 t0 = time.monotonic()
                 enc.submit(bufs[i].array[: n * fb], n)

@@ -74,6 +74,9 @@ extern "C" {
                                   default with -vf scale (measured faster there); this flag forces
                                   it for unscaled input */
 #define MJG_F_DCT_VALU 512u    /* -huffman default: the VALU passes even with -vf scale (A/B) */
+#define MJG_F_NO_MERGE 1024u   /* no library-side merging: every mjg_submit is a launch of its own
+                                  (by default single-segment device submits are held while the GPU
+                                  has a launch queued and launched two at a time, see mjg_submit) */
 
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */
@@ -124,12 +127,19 @@ size_t mjg_frame_bytes(const mjg_ctx *ctx);
 int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 
 /* Encode `nframes` (<= max_batch) packed I420 frames, asynchronously: H2D, scale and
- * k_encode on the submit's stream, the scan/stuff/write tail on the ctx's tail stream
- * after the submit's k_encode.  Up to mjg_queue_depth() submits may be queued (each has its
- * own output and scratch buffers and its own stream): the next one's k_encode runs beside the
- * previous one's drain and tail; MJG_E_STATE with that many queued.  src_is_device = 0: `frames` is host memory (copied H2D through the ctx's
- * staging buffer; pinned memory from mjg_host_alloc() makes this asynchronous);
- * src_is_device = 1: `frames` is device memory on ctx's device, read in place.
+ * k_encode on a launch slot's stream, the scan/stuff/write tail on the ctx's tail stream
+ * after the launch's k_encode.  mjg_queue_depth() launches may be queued (each has its own
+ * output and scratch buffers and its own stream): the next one's k_encode runs beside the
+ * previous one's drain and tail.  src_is_device = 0: `frames` is host memory (copied H2D
+ * through the slot's staging buffer; pinned memory from mjg_host_alloc() makes this
+ * asynchronous), a launch of its own; src_is_device = 1: `frames` is device memory on ctx's
+ * device, read in place.  Library-side merging (unless MJG_F_NO_MERGE / MJG_MERGE=1): a
+ * device submit made while a launch is queued is held and launched together with the next
+ * device submit, as one segment list (mjg_submit_segments' kernels), or alone when the GPU
+ * runs dry or the caller syncs it; each submit stays a job of its own for mjg_sync / mjg_fetch
+ * with exactly the bytes of an unmerged launch.  The frames must stay valid until the job is
+ * synced.  Up to mjg_ctx_queue_depth(ctx) device submits may be pending; MJG_E_STATE past
+ * that (or when no launch slot is free for a host submit).
  * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
 int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
 /* Several segments in one submit: segment k's seg_nframes[k] packed I420 frames at device
@@ -142,7 +152,8 @@ int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_devi
 int mjg_submit_segments(mjg_ctx *ctx, const uint8_t *const *seg_frames, const int *seg_nframes, int nsegs);
 /* Most segments one mjg_submit_segments() may carry (4). */
 int mjg_max_segments(void);
-/* Wait for the oldest queued submit (with none queued: report the last synced one again).
+/* Wait for the oldest pending submit (with none pending: report the last synced one again;
+ * a held one is launched first).
  * frame_sizes (may be NULL) receives its nframes JPEG sizes; *total (may be NULL) the packed
  * total.  Grows the output buffer and re-runs the final kernel if the packed output
  * exceeded its capacity. */
@@ -163,8 +174,13 @@ int mjg_output_device(mjg_ctx *ctx, const uint8_t **data, const uint64_t **offse
  * the caller; the tail kernels run on another stream ordered after k_encode).  Consecutive
  * submits rotate over mjg_queue_depth() such streams. */
 void *mjg_stream(mjg_ctx *ctx);
-/* How many submits mjg_submit queues before one must be synced (2). */
+/* How many launches may be queued before one must be synced (2): the depth for host submits
+ * and mjg_submit_segments, which each take a launch of their own. */
 int mjg_queue_depth(void);
+/* How many single-segment device submits (mjg_submit, src_is_device = 1) ctx holds pending
+ * before one must be synced: mjg_queue_depth() launches of up to two merged submits each (4),
+ * or mjg_queue_depth() when merging is off. */
+int mjg_ctx_queue_depth(const mjg_ctx *ctx);
 
 /* Pinned host memory for mjg_submit / mjg_fetch. */
 int mjg_host_alloc(size_t bytes, void **ptr);

@@ -569,7 +569,7 @@ def test_pipelined_submits():
     frames = rand_frames(w, h, 7, seed=21, kind="smooth")
     ref = oracle_frames(frames, w, h, q, False)
     with MjpegEncoder(0, w, h, qscale=q, max_batch=3) as enc:
-        assert enc.depth == 2
+        assert enc.host_depth == 2 and enc.depth == 4  # host submits: one launch each
         enc.submit(frames[0:3])
         enc.submit(frames[3:5])
         with pytest.raises(MjgError):
@@ -594,6 +594,110 @@ def test_pipelined_submits():
         enc.sync()
         b = enc.fetch()
     assert a + b == oracle_frames(nz, 256, 128, 2, True)
+
+
+MERGE_CFGS = {"default": (200, 120, 200, 120, "default", False), "optimal": (200, 120, 200, 120, "optimal", False),
+              "scale": (240, 136, 120, 68, "default", False), "rst": (200, 120, 200, 120, "default", True)}
+
+
+@pytest.mark.parametrize("cfg", sorted(MERGE_CFGS))
+def test_library_merges_queued_device_submits(cfg):
+    """Library-side merging (mjg_submit, r05): a device submit made while a launch is queued is
+    held and launched together with the next one as a segment list; each submit stays a job of
+    its own.  Seven ragged single-segment submits (separate device buffers) in the bench's
+    pattern and out of it: the first launches alone (idle GPU), pairs merge, a submit synced
+    while held launches alone at its sync, and one made after a full drain launches alone.
+    Every job's sizes and JPEGs byte-equal to the oracle; five launches for seven jobs; a fifth
+    pending submit is refused; merge=False gives one launch per submit and the same bytes."""
+    import torch
+    from ffmpeg_distributed_amd._lib import MjgError
+    sw, sh, dw, dh, huff, rst = MERGE_CFGS[cfg]
+    counts = [3, 2, 3, 1, 3, 2, 3]
+    frames = rand_frames(sw, sh, sum(counts), seed=404, kind="testsrc")
+    ref = oracle_frames(frames, sw, sh, 4, False, dw, dh, huffman=huff, rst=rst)
+    segs, o = [], 0
+    for k in counts:
+        segs.append((torch.from_numpy(frames[o:o + k].copy()).to("cuda:0"), o, k))
+        o += k
+    torch.cuda.synchronize()
+
+    def run(merge):
+        out = {}
+        with MjpegEncoder(0, sw, sh, dw, dh, qscale=4, max_batch=3, huffman=huff, rst=rst, timing=True,
+                          merge=merge) as enc:
+            def sub(j):
+                enc.submit(device_ptr=segs[j][0].data_ptr(), nframes=counts[j])
+
+            def done(j):
+                sizes = enc.sync()
+                out[j] = (list(sizes), enc.fetch())
+            if merge:
+                assert enc.depth == 4 and enc.host_depth == 2
+                for j in range(4):  # [0] alone, [1, 2] merged, 3 held
+                    sub(j)
+                with pytest.raises(MjgError):
+                    sub(4)
+                done(0)
+                sub(4)      # [3, 4] merged
+                done(1)
+                done(2)
+                sub(5)      # held behind [3, 4]
+                done(3)
+                done(4)
+                done(5)     # launched alone when job 4's sync left the GPU nothing queued
+                sub(6)      # idle GPU: launched at once
+                done(6)
+            else:
+                assert enc.depth == 2
+                sub(0)
+                sub(1)
+                for j in range(len(counts)):
+                    done(j)
+                    if j + 2 < len(counts):
+                        sub(j + 2)
+            launches = enc.kernel_times()[1]
+        return out, launches
+
+    for merge, want in ((True, 5), (False, len(counts))):
+        out, launches = run(merge)
+        assert launches == want, (merge, launches)
+        for j, (_, o0, k) in enumerate(segs):
+            sizes, got = out[j]
+            assert sizes == [len(r) for r in ref[o0:o0 + k]], (cfg, merge, j)
+            for i in range(k):
+                assert got[i] == ref[o0 + i], (cfg, merge, j, i, first_diff(got[i], ref[o0 + i]))
+
+
+def test_merged_4k_segments_equal_unmerged():
+    """BASELINE configs[1] segments (120 4K frames) in the bench's pattern (four device submits
+    pending, synced when four are): the merged launches' per-segment bytes equal those of
+    unmerged launches (which test_4k_segment_batch_from_device_memory pins to the oracle)."""
+    import torch
+    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
+    w, h, n = 3840, 2160, 120
+    dev = torch.device("cuda", 0)
+    pools = []
+    for j in range(3):
+        p = torch.empty((n, i420_frame_bytes(w, h)), dtype=torch.uint8, device=dev)
+        for i in range(0, n, 20):
+            p[i:i + 20] = testsrc2_i420_torch(w, h, 5000 + j * n + i, 20, dev)
+        pools.append(p)
+    torch.cuda.synchronize()
+    res = {}
+    for merge in (False, True):
+        got = []
+        with MjpegEncoder(0, w, h, qscale=5, max_batch=n, merge=merge, timing=True) as enc:
+            for s in range(7):
+                enc.submit(device_ptr=pools[s % 3].data_ptr(), nframes=n)
+                if enc.pending == enc.depth:
+                    enc.sync()
+                    got.append(enc.fetch())
+            while enc.pending:
+                enc.sync()
+                got.append(enc.fetch())
+            res[merge] = (got, enc.kernel_times()[1])
+    assert res[False][1] == 7 and res[True][1] == 4  # merged: [0] [1 2] [3 4] [5 6]
+    assert res[True][0] == res[False][0]
 
 
 @pytest.mark.parametrize("cfg", ["optimal", "scale", "scale_optimal", "default"])
