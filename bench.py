@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--huffman", choices=["default", "optimal"], default=None)
     p.add_argument("--rst", action="store_true",
                    help="slice-threaded layout (-slices N: DRI + one restart interval per MCU row)")
+    p.add_argument("--prewarm-ms", type=float, default=0.0,
+                   help="untimed encode launches for this long before the warmup steps (clock ramp probe)")
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--pool", type=int, default=480, help="distinct resident frames per GPU")
@@ -68,6 +70,9 @@ def parse():
     p.add_argument("--cpu-baseline-only", action="store_true",
                    help="internal: run the CPU baseline sweep alone (no torch, no GPU) and print it")
     p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (rank 0, N=1 only)")
+    p.add_argument("--e2e-only", action="store_true",
+                   help="internal: run the end-to-end leg alone (no torch, no GPU in this process) and print it")
+    p.add_argument("--device", type=int, default=0, help="internal (--e2e-only): the GPU of the worker path")
     p.add_argument("--e2e-segments", type=int, default=6)
     p.add_argument("--segments-per-launch", action="store_true",
                    help="also time K = 2, 4 segments per submit (mjg_submit_segments, N=1 only); off by "
@@ -349,6 +354,20 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
     return out
 
 
+def e2e_child(workload: str, device: int, segments: int):
+    """e2e in a fresh interpreter (`bench.py --e2e-only`) that never imports torch or HIP: the
+    dispatcher's process (fd.py:120-148) holds no GPU state, while this benchmark process holds
+    the HIP runtime and a resident frame pool, and forking the per-segment processes off it
+    (subprocess.Popen) costs milliseconds per segment that the dispatcher never pays."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--workload", workload,
+           "--device", str(device), "--e2e-segments", str(segments)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"e2e child exited {r.returncode}: {r.stderr[-1500:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 # ------------------------------------------------------------------------ roofline
 def frame_bytes(w, h):
     return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
@@ -450,6 +469,10 @@ def main():
         res = cpu_baseline_sweep(a.cpu_seconds)
         print(json.dumps(res), flush=True)
         return res
+    if a.e2e_only:  # the child of e2e_child: the dispatcher's side, no GPU in this process
+        res = e2e(a.workload, a.device, a.e2e_segments)
+        print(json.dumps(res), flush=True)
+        return res
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -518,10 +541,18 @@ def main():
 
     def reset():
         drain_and_sync()
-        enc.kernel_times(reset=True)
+        if not a.no_kernel_timing:
+            enc.kernel_times(reset=True)
         bytes_out.clear()
         trace_marker()
 
+    prewarm = 0
+    if a.prewarm_ms > 0:
+        t_pw = time.perf_counter()
+        while (time.perf_counter() - t_pw) * 1e3 < a.prewarm_ms:
+            step(prewarm)
+            prewarm += 1
+        drain_and_sync()
     dt = timed_region(step, a.warmup, a.steps, barrier, drain_and_sync, reset)
     trace_marker()
     if a.no_kernel_timing:
@@ -583,7 +614,7 @@ def main():
         e2e_res = None
         if not a.no_e2e and world == 1 and a.content == "testsrc" and not a.rst and not a.fused:
             try:
-                e2e_res = e2e(a.workload, local, a.e2e_segments)
+                e2e_res = e2e_child(a.workload, local, a.e2e_segments)
             except Exception as e:  # reported, never fatal for the GPU number
                 e2e_res = {"error": repr(e)}
         cpu = None

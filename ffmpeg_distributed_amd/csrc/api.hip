@@ -255,12 +255,14 @@ struct mjg_ctx {
   uint64_t last_off = 0, last_total = 0;  // its packed bytes' offset in the launch's d_out, size
   bool synced_since_submit = false;
   int merge = 1;               // jobs per launch for single-segment device submits (kMerge or 1)
+  bool hold_idle = false;      // hold a lone device job even when the GPU is idle (MJG_MERGE_HOLD=1)
   int held = 0;                // device jobs held for the next launch (0..merge)
   const uint8_t *held_p[kMaxSegs] = {};
   int held_n[kMaxSegs] = {};
   int launches = 0;            // launches since open (tests / diagnostics)
 
   bool timing = false, timing_detail = false;
+  bool timing_tail = false;  // MJG_F_TIMING's tail interval (MJG_TIMING_NOTAIL=1: off, A/B of the events' cost)
   uint8_t *h_fetch = nullptr;  // page-locked copy of the last fetched output (mjg_fetch_host)
   size_t h_fetch_cap = 0;
   double t_acc[MJG_NUM_KERNELS] = {0};
@@ -737,6 +739,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // MJG_MERGE=1 turns it off for a process (A/B), =2..4 sets the jobs per launch
   c->merge = kMerge;
   if (const char *e = getenv("MJG_MERGE")) c->merge = std::max(1, std::min(kMaxSegs, atoi(e)));
+  if (const char *e = getenv("MJG_MERGE_HOLD")) c->hold_idle = atoi(e) != 0;
   if ((k.flags & MJG_F_NO_MERGE) || (k.flags & MJG_F_FUSED)) c->merge = 1;
   if (c->merge > 1) {  // slot buffers for merge * max_batch frames: within a share of free memory
     size_t fr = 0, tot = 0;
@@ -754,6 +757,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->slot_NS = NS;
   c->timing = (k.flags & (MJG_F_TIMING | MJG_F_TIMING_DETAIL)) != 0;
   c->timing_detail = (k.flags & MJG_F_TIMING_DETAIL) != 0;
+  c->timing_tail = c->timing && !c->timing_detail && !(getenv("MJG_TIMING_NOTAIL") && atoi(getenv("MJG_TIMING_NOTAIL")));
   HIP_TRY(hipMemcpy(c->d_tabs, tabs, sizeof tabs, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), c->hdr.size(), hipMemcpyHostToDevice));
 
@@ -864,7 +868,7 @@ int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
       c->optimal ? S.d_hdr_lens : nullptr, (int)c->dht_pos, (int)c->dht_end, S.d_dht,
       c->optimal ? S.d_dht_nval : nullptr, S.d_out, (uint64_t)S.out_cap, S.d_status);
   tmark(c, S, MJG_K_WRITE, 1);
-  if (c->timing && !c->timing_detail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->tail);
+  if (c->timing_tail && !reset_status) (void)hipEventRecord(S.ev[MJG_K_TAIL][1], c->tail);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(S.h_sizes, S.d_frame_size, n * sizeof(uint64_t), hipMemcpyDeviceToHost,
                          c->tail));
@@ -1097,7 +1101,7 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(S.enc_done, S.st));
   HIP_TRY(hipStreamWaitEvent(c->tail, S.enc_done, 0));
-  if (c->timing && !c->timing_detail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->tail);
+  if (c->timing_tail) (void)hipEventRecord(S.ev[MJG_K_TAIL][0], c->tail);
   tmark(c, S, MJG_K_SCAN_BITS, 0);
   const int ndone = 1;  // k_scan_ff's frame ticket
   if (c->rst)
@@ -1176,7 +1180,7 @@ int launch_held(mjg_ctx *c) {
 // mjg_output_device) until the caller's next submit.
 int try_launch_held(mjg_ctx *c, bool at_sync) {
   if (!c->held || c->nout == kSlots) return MJG_OK;
-  if (c->held < c->merge && c->nout > 0) return MJG_OK;
+  if (c->held < c->merge && (c->nout > 0 || c->hold_idle)) return MJG_OK;
   if (at_sync && c->head == c->last) return MJG_OK;
   return launch_held(c);
 }
@@ -1275,6 +1279,7 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
           if (k == MJG_K_HUFF && !c->optimal) continue;
           const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
           if (tail != c->timing_detail && (tail || k == MJG_K_TAIL)) continue;
+          if (k == MJG_K_TAIL && !c->timing_tail) continue;
           float ms = 0.f;
           if (hipEventElapsedTime(&ms, S.ev[k][0], S.ev[k][1]) == hipSuccess) c->t_acc[k] += ms;
         }

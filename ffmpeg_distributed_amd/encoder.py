@@ -234,6 +234,23 @@ class MjpegEncoder:
             o += int(s)
         return out
 
+    def fetch_views(self) -> List[memoryview]:
+        """fetch() with one copy: the packed JPEGs copied once out of the page-locked buffer,
+        returned as memoryview slices (valid as long as the views are referenced)."""
+        if self._queued and not self._synced_since_submit:
+            self.sync()
+        sizes = self._last_sizes
+        data, n = C.c_void_p(), C.c_size_t()
+        check(self._L.mjg_fetch_host(self._h, C.byref(data), C.byref(n)))
+        if int(n.value) != int(sizes.sum()):
+            raise MjgError(_lib.MJG_E_STATE, "fetch size mismatch")
+        mv = memoryview(C.string_at(int(data.value or 0), int(n.value)) if n.value else b"")
+        out, o = [], 0
+        for s in sizes:
+            out.append(mv[o:o + int(s)])
+            o += int(s)
+        return out
+
     def encode(self, frames) -> List[bytes]:
         """Encode host frames (any count; split into max_batch submits)."""
         arr = np.ascontiguousarray(np.asarray(frames, dtype=np.uint8)).reshape(-1)

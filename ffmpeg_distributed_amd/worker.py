@@ -88,6 +88,9 @@ class Progress:
 
 
 READ_THREADS = int(os.environ.get("MJG_READ_THREADS", "4"))
+# page-locked batch buffers per encoder context (MJG_WORKER_BUFFERS): the reader fills one
+# while two submits are queued and a third waits for the sync
+NBUF = max(3, int(os.environ.get("MJG_WORKER_BUFFERS", "4")))
 # MJG_WORKER_TRACE=1: one `mjg-trace:` stderr line per segment with where its time went
 # (reader, submit, sync, fetch, mux) and the process's CPU / NUMA placement.
 TRACE = os.environ.get("MJG_WORKER_TRACE", "0") == "1"
@@ -442,7 +445,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     key = (info.width, info.height, dst_w, dst_h, info.full_range, prof.qscale, sar,
            opts.com_itu601 and not info.full_range, prof.huffman, info.chroma, prof.rst, batch)
-    nbuf = 3
+    nbuf = NBUF
     if cache is not None and cache.get("key") == key:
         enc, bufs = cache["enc"], cache["bufs"]
     else:
@@ -459,9 +462,10 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)
 
-    # three page-locked batches: the reader fills one while two are queued on the GPU (the
+    # NBUF page-locked batches: the reader fills one while two are queued on the GPU (the
     # encoder takes a second submit before the first is synced, so its kernels run back to
-    # back); a batch returns to the reader once its submit is synced.
+    # back); a batch returns to the reader as soon as its submit is synced (the H2D has read
+    # it), before the packets are fetched, so the reader never waits on the fetch.
     fb = enc.frame_bytes
     free: "queue.Queue[int]" = queue.Queue()
     full: "queue.Queue" = queue.Queue()
@@ -528,11 +532,11 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         j, m = queued.pop(0)
         t0 = time.monotonic()
         enc.sync()
+        free.put(j)  # consumed by its H2D: back to the reader before the fetch
         t1 = time.monotonic()
-        packets = enc.fetch()
+        packets = enc.fetch_views()  # one copy out of the page-locked buffer
         tr["sync"] += t1 - t0
         tr["fetch"] += time.monotonic() - t1
-        free.put(j)
         if mux_err:
             raise mux_err[0]
         outq.put((packets, m))
