@@ -58,8 +58,9 @@ def parse():
     p.add_argument("--huffman", choices=["default", "optimal"], default=None)
     p.add_argument("--rst", action="store_true",
                    help="slice-threaded layout (-slices N: DRI + one restart interval per MCU row)")
-    p.add_argument("--prewarm-ms", type=float, default=0.0,
-                   help="untimed encode launches for this long before the warmup steps (clock ramp probe)")
+    p.add_argument("--prewarm-ms", type=float, default=500.0,
+                   help="untimed encode steps for this long before the W warmup steps: the GPU leaves its "
+                        "idle clocks only after ~0.3 s of load (without: c2 -7%%, DESIGN §6); 0 turns it off")
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--pool", type=int, default=480, help="distinct resident frames per GPU")
@@ -246,7 +247,7 @@ def parse_worker_trace(line: str) -> dict:
     out, rest = {}, []
     for tok in line.split()[1:]:
         k, sep, v = tok.partition("=")
-        if k in ("frames", "total", "setup", "read", "submit", "sync", "fetch", "mux", "wait"):
+        if k in ("frames", "total", "setup", "handoff", "client", "read", "submit", "sync", "fetch", "mux", "wait"):
             try:
                 out[k] = float(v)
                 continue
@@ -296,7 +297,7 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
             secs = []
             traces.clear()
             for i in range(n):
-                dst = os.path.join(d, f"out{i % 2}.mkv")
+                dst = os.path.join(d, f"out{i}.mkv")  # a new file per segment, as the dispatcher writes
                 t0 = time.monotonic()
                 rc = run_one(dst)
                 secs.append(time.monotonic() - t0)
@@ -306,26 +307,42 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
             r = {"segments": n, "first_segment_s": round(secs[0], 4),
                  "steady_s_per_segment": round(steady, 4), "fps_steady": round(seg_frames / steady, 1),
                  "seconds": [round(x, 4) for x in secs]}
-            if len(traces) > 1:  # the worker's MJG_WORKER_TRACE phases, median over the steady segments
+            if len(traces) > 1:  # the worker's MJG_WORKER_TRACE phases (and the process's start /
+                # exit as the dispatcher sees them), median over the steady segments
                 keys = [k for k in traces[-1] if isinstance(traces[-1][k], float)]
                 r["worker_trace_median_s"] = {k: round(statistics.median(t[k] for t in traces[1:] if k in t), 4)
                                               for k in keys}
                 r["worker_trace_placement"] = traces[-1].get("placement")
             return r
 
+        class TimedProc(D.FFMPEGProc):
+            """FFMPEGProc noting when each stderr line arrives (start / trace line / exit)."""
+            def _line(self, line):
+                self.times.append((time.monotonic(), line[:16]))
+                super()._line(line)
+
         def per_process(resident):
             argv = D.worker_argv(host, args, resident=resident)
             env = dict(os.environ, MJG_WORKER_TRACE="1")  # one mjg-trace: line per segment (worker.py)
 
             def one(dst):
+                t0 = time.monotonic()
                 with open(seg, "rb") as fi, open(dst, "wb") as fo:
-                    p = D.FFMPEGProc(argv, stdin=fi, stdout=fo, env=env)
+                    p = TimedProc(argv, stdin=fi, stdout=fo, env=env)
+                    p.times = []
                     rc = p.run()
+                t_end = time.monotonic()
                 if rc != 0:
                     sys.stderr.write(p.stderr[-2000:])
                 for line in p.stderr.splitlines():
                     if line.startswith("mjg-trace:"):
                         traces.append(parse_worker_trace(line))
+                if traces and p.times:
+                    first = p.times[0][0]
+                    tr_t = next((t for t, l in p.times if l.startswith("mjg-trace")), None)
+                    traces[-1]["client_first_line"] = first - t0  # process start .. the worker's Duration line
+                    if tr_t is not None:
+                        traces[-1]["client_after_trace"] = t_end - tr_t  # the worker's last line .. process exit
                 return rc
             return one
 
@@ -632,6 +649,9 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "prewarm": {"ms": a.prewarm_ms, "steps": prewarm,
+                        "why": "untimed steps before the W warmup steps: the GPU runs at its idle clocks "
+                               "for the first ~0.3 s of load (DESIGN §6)"},
             "ms_per_step": round(dt / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",

@@ -525,6 +525,12 @@ class MkvWriter:
         self._cluster_bytes += len(head) + len(jpeg)
         self.n += 1
 
+    def flush_pending(self):
+        """End the current cluster now and write it (its packets may live in a buffer the
+        caller reuses next: the worker's page-locked output buffers).  Clusters then follow the
+        submits (at most 1 s / 256 frames still holds)."""
+        self._flush()
+
     def _flush(self):
         if self._cluster:
             ts = uint_el(TIMESTAMP, self._cluster_ts)

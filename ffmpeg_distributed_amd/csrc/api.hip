@@ -255,7 +255,7 @@ struct mjg_ctx {
   uint64_t last_off = 0, last_total = 0;  // its packed bytes' offset in the launch's d_out, size
   bool synced_since_submit = false;
   int merge = 1;               // jobs per launch for single-segment device submits (kMerge or 1)
-  bool hold_idle = false;      // hold a lone device job even when the GPU is idle (MJG_MERGE_HOLD=1)
+  bool hold_idle = true;       // hold a lone device job even on an idle GPU (MJG_MERGE_HOLD=0: launch it)
   int held = 0;                // device jobs held for the next launch (0..merge)
   const uint8_t *held_p[kMaxSegs] = {};
   int held_n[kMaxSegs] = {};
@@ -1174,10 +1174,13 @@ int launch_held(mjg_ctx *c) {
   return MJG_OK;
 }
 
-// Launch the held jobs when a launch slot is free and either they are `merge` jobs or the GPU
-// has nothing else queued (a lone job is never held back from an idle GPU).  At mjg_sync the
-// slot of the job just synced stays untouched: its results are read (mjg_fetch,
-// mjg_output_device) until the caller's next submit.
+// Launch the held jobs when a launch slot is free and they are `merge` jobs (with hold_idle off,
+// also when the GPU has nothing else queued); a lone held job launches at its own mjg_sync (or
+// before a host submit).  Holding even on an idle GPU keeps every launch of a stream of device
+// submits a full pair: A/B with prewarmed clocks (profiles/r05_merge_ab.txt) c5 +6%, c1 +3.5%,
+// c4 +1.5%, c2 +0-1% against no merging; launching a lone job on an idle GPU made the first
+// launch a single and lost that gain on c2.  At mjg_sync the slot of the job just synced stays
+// untouched: its results are read (mjg_fetch, mjg_output_device) until the caller's next submit.
 int try_launch_held(mjg_ctx *c, bool at_sync) {
   if (!c->held || c->nout == kSlots) return MJG_OK;
   if (c->held < c->merge && (c->nout > 0 || c->hold_idle)) return MJG_OK;
@@ -1340,7 +1343,8 @@ int mjg_fetch_host(mjg_ctx *c, const uint8_t **data, size_t *len) {
   return MJG_OK;
 }
 
-// mjg_fetch_host, then a copy into the caller's memory.
+// The last synced job's packed JPEGs into the caller's memory: one DMA when it is page-locked
+// (mjg_host_alloc), else mjg_fetch_host and a copy.
 int mjg_fetch(mjg_ctx *c, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
   if (pending_jobs(c) > 0 && !c->synced_since_submit) {
@@ -1349,6 +1353,15 @@ int mjg_fetch(mjg_ctx *c, uint8_t *out, size_t cap) {
   }
   if (c->last < 0) return set_err(MJG_E_STATE, "nothing submitted");
   if (cap < c->last_total) return set_err(MJG_E_CAPACITY, "fetch needs %llu bytes", (unsigned long long)c->last_total);
+  HIP_TRY(hipSetDevice(c->device));
+  // page-locked caller memory (mjg_host_alloc): one DMA straight into it, no staging copy
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost) {
+    if (c->last_total)
+      HIP_TRY(hipMemcpy(out, c->slot[c->last].d_out + c->last_off, c->last_total, hipMemcpyDeviceToHost));
+    return MJG_OK;
+  }
+  (void)hipGetLastError();  // pageable memory: not a HIP pointer
   const uint8_t *p = nullptr;
   size_t n = 0;
   const int rc = mjg_fetch_host(c, &p, &n);

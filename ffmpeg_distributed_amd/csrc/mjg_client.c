@@ -249,6 +249,18 @@ int main(int argc, char **argv) {
   char logp[4400] = "", ldir[64];
   if (log_dir(ldir, sizeof ldir) == 0) snprintf(logp, sizeof logp, "%s/%s.log", ldir, name);
 
+  // with MJG_WORKER_TRACE=1 the start time goes along (MJG_CLIENT_T0, CLOCK_MONOTONIC ns): the
+  // encoder's trace line then splits process start + hand-off from the encode (worker.py)
+  {
+    const char *t = getenv("MJG_WORKER_TRACE");
+    if (t && !strcmp(t, "1")) {
+      struct timespec ts;
+      clock_gettime(CLOCK_MONOTONIC, &ts);
+      char v[32];
+      snprintf(v, sizeof v, "%lld", (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec);
+      setenv("MJG_CLIENT_T0", v, 1);
+    }
+  }
   // request: header, arguments, MJG_* environment
   size_t len = 20, nargs = (size_t)(argc - a), nenv = 0;
   for (int i = a; i < argc; i++) len += strlen(argv[i]) + 1;

@@ -251,6 +251,27 @@ class MjpegEncoder:
             o += int(s)
         return out
 
+    def fetch_into(self, buf: "PinnedBuffer") -> List[memoryview]:
+        """The packed JPEGs of the last synced submit DMA'd straight into `buf` (page-locked,
+        PinnedBuffer: mjg_fetch's one-DMA path, no host copy), returned as memoryview slices of
+        it; MjgError(MJG_E_CAPACITY) when `buf` is too small (see last_total)."""
+        if self._queued and not self._synced_since_submit:
+            self.sync()
+        sizes = self._last_sizes
+        total = int(sizes.sum())
+        check(self._L.mjg_fetch(self._h, C.c_void_p(buf.ptr), int(buf.nbytes)))
+        mv = memoryview(buf.array)[:total]
+        out, o = [], 0
+        for s in sizes:
+            out.append(mv[o:o + int(s)])
+            o += int(s)
+        return out
+
+    @property
+    def last_total(self) -> int:
+        """Packed bytes of the last synced submit."""
+        return int(self._last_sizes.sum())
+
     def encode(self, frames) -> List[bytes]:
         """Encode host frames (any count; split into max_batch submits)."""
         arr = np.ascontiguousarray(np.asarray(frames, dtype=np.uint8)).reshape(-1)

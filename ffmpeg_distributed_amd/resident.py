@@ -134,7 +134,7 @@ class Resident:
         for c in extra:
             worker.release(c)
 
-    def handle(self, conn: socket.socket):
+    def handle(self, conn: socket.socket, t_accept: float = 0.0):
         fds: List[int] = []
         rc = 1
         try:
@@ -149,7 +149,7 @@ class Resident:
             elif len(fds) != 3:
                 rc = 1
             else:
-                rc = self._encode(args, env, fds)
+                rc = self._encode(args, env, fds, t_accept)
                 fds = []  # closed by _encode
             conn.sendall(struct.pack("<i", rc))
         except (OSError, ValueError, EOFError) as e:
@@ -162,7 +162,7 @@ class Resident:
                 self.active -= 1
                 self.last = time.monotonic()
 
-    def _encode(self, args: List[str], env: Dict[str, str], fds: List[int]) -> int:
+    def _encode(self, args: List[str], env: Dict[str, str], fds: List[int], t_accept: float = 0.0) -> int:
         fin = os.fdopen(fds[0], "rb")
         fout = os.fdopen(fds[1], "wb")
         ferr = io.TextIOWrapper(os.fdopen(fds[2], "wb"), encoding="utf-8", errors="replace",
@@ -170,7 +170,7 @@ class Resident:
         cache = self._take_cache()
         rc = 1
         try:
-            opts = worker.Options.from_env(env, worker.SERVE_BATCH_BYTES)
+            opts = worker.Options.from_env(env, worker.SERVE_BATCH_BYTES, t_accept=t_accept)
             rc = self.run(self.device, args, stdin=fin, stdout=fout, stderr=ferr, cache=cache, opts=opts)
         except Exception as e:  # a failed segment: the dispatcher re-queues it
             try:
@@ -194,6 +194,7 @@ class Resident:
             while not self.stop.is_set():
                 try:
                     conn, _ = self.sock.accept()
+                    t_accept = time.monotonic()
                 except socket.timeout:
                     with self.lock:
                         if self.active == 0 and time.monotonic() - self.last > self.idle:
@@ -202,7 +203,7 @@ class Resident:
                 conn.settimeout(None)
                 with self.lock:
                     self.active += 1
-                t = threading.Thread(target=self.handle, args=(conn,), daemon=True)
+                t = threading.Thread(target=self.handle, args=(conn, t_accept), daemon=True)
                 self.threads = [x for x in self.threads if x.is_alive()] + [t]
                 t.start()
         finally:

@@ -87,10 +87,12 @@ class Progress:
         self.err.flush()
 
 
-READ_THREADS = int(os.environ.get("MJG_READ_THREADS", "4"))
+# 8: 84 GB/s from the page cache for a 4K segment against 61 GB/s with 4 (r05, bench e2e trace)
+READ_THREADS = int(os.environ.get("MJG_READ_THREADS", "8"))
 # page-locked batch buffers per encoder context (MJG_WORKER_BUFFERS): the reader fills one
 # while two submits are queued and a third waits for the sync
 NBUF = max(3, int(os.environ.get("MJG_WORKER_BUFFERS", "4")))
+NOUT = 6  # page-locked output buffers: one being filled, up to four queued to the muxer, one in its write
 # MJG_WORKER_TRACE=1: one `mjg-trace:` stderr line per segment with where its time went
 # (reader, submit, sync, fetch, mux) and the process's CPU / NUMA placement.
 TRACE = os.environ.get("MJG_WORKER_TRACE", "0") == "1"
@@ -104,17 +106,23 @@ class Options:
     batch: int = 0                  # MJG_WORKER_BATCH: frames per submit (0: by bytes)
     batch_bytes: int = 96 << 20     # MJG_WORKER_BATCH_BYTES
     com_itu601: bool = False        # MJG_COM_ITU601
-    read_threads: int = 4           # MJG_READ_THREADS
+    read_threads: int = 8           # MJG_READ_THREADS
     trace: bool = False             # MJG_WORKER_TRACE
+    client_t0: float = 0.0          # trace: the mjg_client's start (MJG_CLIENT_T0, monotonic ns)
+    t_accept: float = 0.0           # trace: when the resident encoder accepted the request
 
     @classmethod
-    def from_env(cls, env, batch_bytes: Optional[int] = None) -> "Options":
+    def from_env(cls, env, batch_bytes: Optional[int] = None, t_accept: float = 0.0) -> "Options":
         """From NAME=VALUE settings (absent names take the defaults above)."""
+        try:
+            client_t0 = int(env.get("MJG_CLIENT_T0", "0") or 0) / 1e9
+        except ValueError:
+            client_t0 = 0.0
         return cls(batch=int(env.get("MJG_WORKER_BATCH", "0") or 0),
                    batch_bytes=int(env.get("MJG_WORKER_BATCH_BYTES", "0") or 0) or batch_bytes or (96 << 20),
                    com_itu601=env.get("MJG_COM_ITU601", "0") == "1",
-                   read_threads=max(1, int(env.get("MJG_READ_THREADS", "4") or 4)),
-                   trace=env.get("MJG_WORKER_TRACE", "0") == "1")
+                   read_threads=max(1, int(env.get("MJG_READ_THREADS", "8") or 8)),
+                   trace=env.get("MJG_WORKER_TRACE", "0") == "1", client_t0=client_t0, t_accept=t_accept)
 
 
 def process_options(batch_bytes: Optional[int] = None) -> Options:
@@ -447,7 +455,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
            opts.com_itu601 and not info.full_range, prof.huffman, info.chroma, prof.rst, batch)
     nbuf = NBUF
     if cache is not None and cache.get("key") == key:
-        enc, bufs = cache["enc"], cache["bufs"]
+        enc, bufs, obufs = cache["enc"], cache["bufs"], cache["obufs"]
     else:
         if cache is not None:
             release(cache)
@@ -456,8 +464,11 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
                            com_itu601=opts.com_itu601 and not info.full_range, huffman=prof.huffman,
                            chroma=info.chroma, rst=prof.rst)
         bufs = [PinnedBuffer(batch * enc.frame_bytes) for _ in range(nbuf)]
+        # page-locked output buffers: the packets are DMA'd into one (enc.fetch_into) and the
+        # muxer writes them from it; regrown when a submit's JPEGs do not fit
+        obufs = [None] * NOUT
         if cache is not None:
-            cache.update(key=key, enc=enc, bufs=bufs)
+            cache.update(key=key, enc=enc, bufs=bufs, obufs=obufs)
     prog = Progress(stderr, info.fps, prof.qscale)
     prog.duration(src.duration)
     mkv = container.MkvWriter(stdout, dst_w, dst_h, info.fps, sar)
@@ -499,6 +510,9 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     # the muxer thread writes each synced submit's packets while the main thread keeps the
     # GPU fed (a 4K segment's 120 JPEGs are ~20 MB of writes)
     outq: "queue.Queue" = queue.Queue(maxsize=4)
+    ofree: "queue.Queue[int]" = queue.Queue()  # output buffers the muxer has written
+    for i in range(NOUT):
+        ofree.put(i)
     mux_err: list = []
 
     def muxer():
@@ -512,18 +526,21 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
                 continue
             if item is None:
                 return
+            packets, m, ob = item
             if mux_err:
+                ofree.put(ob)
                 continue  # drain after a failure
-            packets, m = item
             try:
                 t0 = time.monotonic()
                 for p in packets:
                     mkv.write_frame(p)
+                mkv.flush_pending()  # the packets leave buffer `ob` before it is reused
                 tr["mux"] += time.monotonic() - t0
                 frames += m
                 prog.update(frames, sum(len(p) for p in packets))
             except BaseException as e:  # surfaced by the main thread
                 mux_err.append(e)
+            ofree.put(ob)
 
     mt = threading.Thread(target=muxer, daemon=True)
     mt.start()
@@ -534,12 +551,24 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         enc.sync()
         free.put(j)  # consumed by its H2D: back to the reader before the fetch
         t1 = time.monotonic()
-        packets = enc.fetch_views()  # one copy out of the page-locked buffer
+        while True:  # a written output buffer (the muxer returns them); abort: error path
+            try:
+                ob = ofree.get(timeout=0.1)
+                break
+            except queue.Empty:
+                if mux_err:
+                    raise mux_err[0]
+        need = enc.last_total
+        if obufs[ob] is None or obufs[ob].nbytes < need:
+            if obufs[ob] is not None:
+                obufs[ob].free()
+            obufs[ob] = PinnedBuffer(max(need + need // 2, 1 << 20))
+        packets = enc.fetch_into(obufs[ob])  # one DMA into page-locked memory, no copy
         tr["sync"] += t1 - t0
         tr["fetch"] += time.monotonic() - t1
         if mux_err:
             raise mux_err[0]
-        outq.put((packets, m))
+        outq.put((packets, m, ob))
 
     failed = True
     try:
@@ -571,8 +600,13 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         prog.update(frames, 0, final=True)
         failed = False
         if opts.trace:
+            hand = ""  # the resident's hand-off: client start -> accept -> worker.run
+            if opts.t_accept:
+                hand += f"handoff={t_run - opts.t_accept:.4f} "
+                if opts.client_t0:
+                    hand += f"client={opts.t_accept - opts.client_t0:.4f} "
             stderr.write(f"mjg-trace: frames={frames} total={time.monotonic() - t_seg:.4f} "
-                         f"setup={t_seg - t_run:.4f} "
+                         f"setup={t_seg - t_run:.4f} {hand}"
                          + " ".join(f"{k}={v:.4f}" for k, v in tr.items()) + f" {placement()}\n")
             stderr.flush()
     finally:
@@ -595,13 +629,13 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
         stuck = th.is_alive()  # blocked on a stdin pipe that never delivers: leak, never free
         rc = src.close(kill=failed)
         if (failed or stuck) and cache is not None:  # a submit may still be queued: start afresh
-            for k in ("key", "enc", "bufs"):
+            for k in ("key", "enc", "bufs", "obufs"):
                 cache.pop(k, None)
             cache = None
         if cache is None:
             enc.close()
             if not stuck:
-                for b in bufs:
+                for b in bufs + [b for b in obufs if b is not None]:
                     b.free()
     if rc:
         stderr.write(f"decoder exited with {rc}\n")
@@ -612,10 +646,11 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
 def release(cache) -> None:
     """Close the encoder context and free the batch buffers a serve cache holds."""
     enc, bufs = cache.pop("enc", None), cache.pop("bufs", None) or []
+    obufs = [b for b in (cache.pop("obufs", None) or []) if b is not None]
     cache.pop("key", None)
     if enc is not None:
         enc.close()
-    for b in bufs:
+    for b in bufs + obufs:
         b.free()
 
 

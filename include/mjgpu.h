@@ -160,8 +160,8 @@ int mjg_max_segments(void);
 int mjg_sync(mjg_ctx *ctx, uint64_t *frame_sizes, uint64_t *total);
 /* Copy the packed JPEGs of the last synced submit (frame after frame) to host memory; syncs
  * the oldest queued submit first when mjg_sync was not called since the last mjg_submit.
- * The bytes go through the context's page-locked buffer (mjg_fetch_host) and are then copied
- * into `out`: one host copy more than mjg_fetch_host, which avoids it. */
+ * Page-locked `out` (from mjg_host_alloc) receives them by one DMA; pageable memory through
+ * the context's page-locked buffer (mjg_fetch_host) and one host copy. */
 int mjg_fetch(mjg_ctx *ctx, uint8_t *out, size_t cap);
 /* The same bytes without the copy into caller memory: *data points at the context's
  * page-locked copy (DMA'd from the device), *len its size; valid until the next

@@ -602,13 +602,13 @@ MERGE_CFGS = {"default": (200, 120, 200, 120, "default", False), "optimal": (200
 
 @pytest.mark.parametrize("cfg", sorted(MERGE_CFGS))
 def test_library_merges_queued_device_submits(cfg):
-    """Library-side merging (mjg_submit, r05): a device submit made while a launch is queued is
-    held and launched together with the next one as a segment list; each submit stays a job of
-    its own.  Seven ragged single-segment submits (separate device buffers) in the bench's
-    pattern and out of it: the first launches alone (idle GPU), pairs merge, a submit synced
-    while held launches alone at its sync, and one made after a full drain launches alone.
-    Every job's sizes and JPEGs byte-equal to the oracle; five launches for seven jobs; a fifth
-    pending submit is refused; merge=False gives one launch per submit and the same bytes."""
+    """Library-side merging (mjg_submit, r05): a device submit is held and launched together with
+    the next one as a segment list; each submit stays a job of its own.  Seven ragged
+    single-segment submits (separate device buffers) in the bench's pattern and out of it: pairs
+    merge, a held job is launched with its partner or alone at its own sync.  Every job's sizes
+    and JPEGs byte-equal to the oracle; four launches for seven jobs ([0 1] [2 3] [4 5] [6]); a
+    fifth pending submit is refused; merge=False gives one launch per submit and the same
+    bytes."""
     import torch
     from ffmpeg_distributed_amd._lib import MjgError
     sw, sh, dw, dh, huff, rst = MERGE_CFGS[cfg]
@@ -633,20 +633,20 @@ def test_library_merges_queued_device_submits(cfg):
                 out[j] = (list(sizes), enc.fetch())
             if merge:
                 assert enc.depth == 4 and enc.host_depth == 2
-                for j in range(4):  # [0] alone, [1, 2] merged, 3 held
+                for j in range(4):  # [0, 1] and [2, 3] merged
                     sub(j)
                 with pytest.raises(MjgError):
                     sub(4)
                 done(0)
-                sub(4)      # [3, 4] merged
+                sub(4)      # held
                 done(1)
                 done(2)
-                sub(5)      # held behind [3, 4]
+                sub(5)      # [4, 5] merged
                 done(3)
                 done(4)
-                done(5)     # launched alone when job 4's sync left the GPU nothing queued
-                sub(6)      # idle GPU: launched at once
-                done(6)
+                done(5)
+                sub(6)      # held on the idle GPU
+                done(6)     # launched alone at its own sync
             else:
                 assert enc.depth == 2
                 sub(0)
@@ -658,7 +658,7 @@ def test_library_merges_queued_device_submits(cfg):
             launches = enc.kernel_times()[1]
         return out, launches
 
-    for merge, want in ((True, 5), (False, len(counts))):
+    for merge, want in ((True, 4), (False, len(counts))):
         out, launches = run(merge)
         assert launches == want, (merge, launches)
         for j, (_, o0, k) in enumerate(segs):
@@ -696,7 +696,7 @@ def test_merged_4k_segments_equal_unmerged():
                 enc.sync()
                 got.append(enc.fetch())
             res[merge] = (got, enc.kernel_times()[1])
-    assert res[False][1] == 7 and res[True][1] == 4  # merged: [0] [1 2] [3 4] [5 6]
+    assert res[False][1] == 7 and res[True][1] == 4  # merged: [0 1] [2 3] [4 5] [6]
     assert res[True][0] == res[False][0]
 
 

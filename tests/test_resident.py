@@ -48,7 +48,7 @@ def test_options_from_request_env():
     from ffmpeg_distributed_amd import worker
     o = worker.Options.from_env({"MJG_WORKER_TRACE": "1", "MJG_WORKER_BATCH": "3",
                                  "MJG_COM_ITU601": "1"}, 256 << 20)
-    assert o.trace and o.batch == 3 and o.com_itu601 and o.batch_bytes == 256 << 20 and o.read_threads == 4
+    assert o.trace and o.batch == 3 and o.com_itu601 and o.batch_bytes == 256 << 20 and o.read_threads == 8
     assert worker.Options.from_env({}) == worker.Options()
 
 
