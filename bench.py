@@ -78,8 +78,6 @@ def parse():
     p.add_argument("--segments-per-launch", action="store_true",
                    help="also time K = 2, 4 segments per submit (mjg_submit_segments, N=1 only); off by "
                         "default so a profile of the default command holds only the headline's launches")
-    p.add_argument("--fused", action="store_true",
-                   help="-vf scale configs: the opt-in fused k_scale_encode instead of k_scale + k_encode")
     p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
                    help="-huffman default: k_encode's DCT stage (auto: the matrix cores with -vf scale)")
     p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
@@ -438,7 +436,7 @@ def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
     src_b, dst_b, jpeg_b = frame_bytes(W, H) * fpl, frame_bytes(DW, DH) * fpl, mean_jpeg * fpl
     sstep = (seg or fpl) / fpl  # one step's share of a launch's bytes
     out = []
-    if scaled and kt.get("scale", 0) > 0:  # unfused: k_scale writes the scaled planes to HBM
+    if scaled:  # k_scale writes the scaled planes to HBM, k_encode reads them
         out.append(roofline_entry("k_scale", src_b + dst_b, kt["scale"], pmc_traffic(pmc, fpl, "k_scale"),
                                   "source planes read + scaled planes written"))
         enc_in = dst_b
@@ -456,7 +454,7 @@ def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
                                  pmc_traffic(pmc, fpl, "k_encode", "k_huff_build", "k_emit_syms"),
                                  "input planes read + JPEG written")
     else:
-        name = "k_encode" if not (scaled and kt.get("scale", 0) == 0) else "k_scale_encode (fused)"
+        name = "k_encode"
         out.append(roofline_entry(name, enc_in + jpeg_b, kt["encode"],
                                   pmc_traffic(pmc, fpl, "k_encode", "k_scale_encode"),
                                   ("scaled" if enc_in == dst_b and scaled else "input") +
@@ -530,7 +528,7 @@ def main():
 
     enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg,
                        timing=False if a.no_kernel_timing else ("detail" if a.kernel_timing_detail else True),
-                       huffman=HUFF, rst=a.rst, fused=a.fused,
+                       huffman=HUFF, rst=a.rst,
                        dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
     bytes_out = []
 
@@ -584,7 +582,7 @@ def main():
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
     fpl = a.steps * seg / nl if nl else seg  # frames per launch (merged launches carry two segments)
     pmc, pmc_src = (load_pmc(a.workload, a.content, B.source_digest())
-                    if (seg == SEG and not a.rst and not a.fused and a.dct == "auto"
+                    if (seg == SEG and not a.rst and a.dct == "auto"
                         and HUFF == WORKLOADS[a.workload][7]) else ({}, "no PMC pass for this configuration"))
     overlap = True  # consecutive launches run on two streams (csrc/api.hip alloc_slot; see rooflines)
     primary, per_kernel = rooflines(kt, fpl, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H),
@@ -596,7 +594,7 @@ def main():
     # submit to an idle GPU launches at once) and two segments per launch (the shape of a
     # merged launch, as one two-segment list on a context of twice the frames)
     iso = []
-    if not a.no_kernel_timing and not a.fused:
+    if not a.no_kernel_timing:
         for k in (1, 2):
             if k > nseg_pool:
                 continue
@@ -623,13 +621,13 @@ def main():
         trace_marker()
 
     batched = None
-    if a.segments_per_launch and world == 1 and not a.fused and not a.rst and nseg_pool >= 2:
+    if a.segments_per_launch and world == 1 and not a.rst and nseg_pool >= 2:
         batched = segments_per_launch(a, pool, seg, nseg_pool, W, H, DW, DH, FULL, Q, HUFF, local)
 
     out = None
     if rank == 0:
         e2e_res = None
-        if not a.no_e2e and world == 1 and a.content == "testsrc" and not a.rst and not a.fused:
+        if not a.no_e2e and world == 1 and a.content == "testsrc" and not a.rst:
             try:
                 e2e_res = e2e_child(a.workload, local, a.e2e_segments)
             except Exception as e:  # reported, never fatal for the GPU number
@@ -665,7 +663,7 @@ def main():
                        "profile": (f"-vf scale={DW}:{DH}:flags=bicubic " if (DW, DH) != (W, H) else "")
                        + f"-c:v mjpeg -q:v {Q} -dct int -huffman {HUFF} -bitexact"
                        + (" -slices 8" if a.rst else ""),
-                       **({"scale_kernels": "k_scale_encode (fused)" if a.fused else "k_scale + k_encode"}
+                       **({"scale_kernels": "k_scale + k_encode"}
                           if (DW, DH) != (W, H) else {}),
                        "dct": "VALU (k_encode<.., optimal counting pass>)" if HUFF == "optimal" else
                               ("matrix cores (dct_mfma)" if a.dct == "mfma" or (a.dct == "auto" and (DW, DH) != (W, H))

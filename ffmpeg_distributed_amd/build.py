@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libmjgpu.so")
 STAMP = LIB + ".sha256"
 SOURCES = ["api.hip", "sws_filter.cpp"]
-DEPS = SOURCES + ["kernels.hip", "scale.hip", "fused.hip", "jpeg_tables.h", "sws_filter.h"]
+DEPS = SOURCES + ["kernels.hip", "scale.hip", "jpeg_tables.h", "sws_filter.h"]
 ARCH = os.environ.get("MJG_OFFLOAD_ARCH", "gfx950")
 
 

@@ -16,7 +16,6 @@
 #include "jpeg_tables.h"
 #include "kernels.hip"
 #include "scale.hip"
-#include "fused.hip"
 #include "sws_filter.h"
 
 using namespace mjg;
@@ -158,11 +157,6 @@ struct PlaneScale {
   size_t lds = 0;
   dim3 grid;
   int th = 32;  // k_scale tile height (64: the 2:1 filters, scale.hip)
-  // k_scale_encode tables (kFusedTabWords per entry): h per scaled column: D4 words, [6] tap
-  // position, [7] tap sum; v per scaled row: [0] first row pair, [1..npv] coefficient pairs
-  uint32_t *d_fh = nullptr, *d_fv = nullptr;
-  std::vector<uint32_t> fh, fv;
-  bool fusable = false;  // taps fit the fused kernel (HT 4/8, D4, windows inside the rows)
 };
 
 // Per-submit state.  A context has kSlots slots so further mjg_submits can be queued before
@@ -236,15 +230,12 @@ struct mjg_ctx {
 
   uint32_t *d_tabs = nullptr;
   uint8_t *d_hdr = nullptr;
-  size_t stage_cols = 0;       // staging columns per slot (persistent waves of k_encode / k_emit_syms / fused)
+  size_t stage_cols = 0;       // staging columns per slot (persistent waves of k_encode / k_emit_syms)
   bool rst = false;            // RST mode (MJG_F_RST, more than one MCU row)
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
-  bool fused = false;   // -vf scale through k_scale_encode (no d_scaled)
   bool dct_mfma = false;  // k_encode's DCT stage on the matrix cores (dct_mfma)
-  FusedGeom fgeom{};
-  int fused_grid = 0;   // persistent k_scale_encode workgroups
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
 
   Slot slot[kSlots];
@@ -280,8 +271,7 @@ void free_ctx(mjg_ctx *c) {
   if (c->tail) (void)hipStreamSynchronize(c->tail);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
-                  c->ps[0].hsum, c->ps[1].hsum, c->ps[1].vps, c->ps[0].d_fh, c->ps[0].d_fv,
-                  c->ps[1].d_fh, c->ps[1].d_fv};
+                  c->ps[0].hsum, c->ps[1].hsum, c->ps[1].vps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
@@ -367,20 +357,6 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
       vcp[(size_t)y * npv + k] = (int32_t)((uint32_t)c0 | ((uint32_t)c1 << 16));
     }
   }
-  // fused tables
-  p.fusable = p.d4 && (ht == 8 || ht == 4) && npv <= ht / 2 + 1;  // v pairs zero-padded to HT/2 + 1
-  p.fh.assign((size_t)dw * kFusedTabWords, 0u);
-  p.fv.assign((size_t)dh * kFusedTabWords, 0u);
-  for (int x = 0; x < dw; x++) {
-    for (int k = 0; k < ht / 2 && k < 6; k++) p.fh[(size_t)x * kFusedTabWords + k] = (uint32_t)hcp[(size_t)x * (ht / 2) + k];
-    p.fh[(size_t)x * kFusedTabWords + 6] = (uint32_t)p.hf.pos[x];
-    p.fh[(size_t)x * kFusedTabWords + 7] = (uint32_t)hsum[x];
-    if (p.hf.pos[x] + ht > sw) p.fusable = false;  // the 8-byte tap window stays inside its row
-  }
-  for (int y = 0; y < dh; y++) {
-    p.fv[(size_t)y * kFusedTabWords] = (uint32_t)vps[y];
-    for (int k = 0; k < npv && k < 7; k++) p.fv[(size_t)y * kFusedTabWords + 1 + k] = (uint32_t)vcp[(size_t)y * npv + k];
-  }
   // k_scale's tile height: 64 rows for the 2:1 filters when every window fits the fast path
   // at a 36-dword row stride (scale.hip), else 32
   auto tile_pairs = [&](int th) {
@@ -441,7 +417,7 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   // launches).  Each launch's own event interval then includes its neighbour's overlap.
   S.st = slot_stream(c, (int)(&S - c->slot));
   if ((rc = dmalloc(&S.d_stage_bits, c->stage_cols * 64 * kStageWords))) return rc;
-  if (c->scale && !c->fused && (rc = dmalloc(&S.d_scaled, B * c->enc_frame_bytes))) return rc;
+  if (c->scale && (rc = dmalloc(&S.d_scaled, B * c->enc_frame_bytes))) return rc;
   if ((rc = dmalloc(&S.d_scratch, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&S.d_stream, B * NC * (size_t)kSlotWords)) ||
       (rc = dmalloc(&S.d_chunk_bits, B * NC)) || (rc = dmalloc(&S.d_chunk_off, B * NC)) ||
@@ -735,12 +711,12 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   }
 
   const size_t NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
-  // merging (kMerge): not with the opt-in fused kernel (no segment lists) or MJG_F_NO_MERGE;
+  // merging (kMerge): off with MJG_F_NO_MERGE;
   // MJG_MERGE=1 turns it off for a process (A/B), =2..4 sets the jobs per launch
   c->merge = kMerge;
   if (const char *e = getenv("MJG_MERGE")) c->merge = std::max(1, std::min(kMaxSegs, atoi(e)));
   if (const char *e = getenv("MJG_MERGE_HOLD")) c->hold_idle = atoi(e) != 0;
-  if ((k.flags & MJG_F_NO_MERGE) || (k.flags & MJG_F_FUSED)) c->merge = 1;
+  if (k.flags & MJG_F_NO_MERGE) c->merge = 1;
   if (c->merge > 1) {  // slot buffers for merge * max_batch frames: within a share of free memory
     size_t fr = 0, tot = 0;
     HIP_TRY(hipMemGetInfo(&fr, &tot));
@@ -778,50 +754,9 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       sg.d_fstride = (long long)c->enc_frame_bytes;
       sg.range = k.in_full_range ? 0 : (p ? 2 : 1);
     }
-    // k_scale_encode: 4:2:0, one entropy-coded segment per frame (its 32-MCU groups are whole
-    // chunks), filters it handles (HT 8 / 4 with D4 coefficients), row pairs within its
-    // h-buffer, and only when MJG_F_FUSED asks for it; otherwise k_scale + k_encode
-    // (>= 32 MCUs per row: a group touches at most two MCU rows, whose v rows are staged in LDS)
-    c->fused = cf == MJG_CHROMA_420 && !c->rst && (k.flags & MJG_F_FUSED) && !(k.flags & MJG_F_DEBUG_COEFS) &&
-               c->ps[0].fusable && c->ps[1].fusable && c->ps[0].g.htaps == c->ps[1].g.htaps &&
-               g.mbw >= kGroupMcus;
-    if (c->fused) {
-      FusedGeom &fg = c->fgeom;
-      for (int p = 0; p < 2; p++) {
-        const ScaleGeom &sg = c->ps[p].g;
-        fg.sw[p] = sg.sw;
-        fg.sh[p] = sg.sh;
-        fg.dw[p] = sg.dw;
-        fg.dh[p] = sg.dh;
-        const int rows = p ? 8 : 16;  // scaled rows per MCU row
-        int np = 0;
-        for (int y0 = 0; y0 < sg.dh; y0 += rows) {
-          const int ya = y0, yb = std::min(y0 + rows - 1, sg.dh - 1);
-          np = std::max(np, (int)c->ps[p].fv[(size_t)yb * kFusedTabWords] + sg.htaps / 2 + 1 -
-                                (int)c->ps[p].fv[(size_t)ya * kFusedTabWords]);
-        }
-        np = (np + 1) & ~1;  // whole batches of 4 pairs plus a tail of 2 (extra rows: clamped, unused)
-        fg.npairs[p] = np;
-        if (np > kFusedMaxPairs) c->fused = false;
-      }
-      fg.s_fstride = (long long)c->in_frame_bytes;
-      fg.s_off[0] = 0;
-      fg.s_off[1] = (long long)k.src_w * k.src_h;
-      fg.s_off[2] = fg.s_off[1] + (long long)scw * sch;
-      fg.gpf = (g.nmcu + kGroupMcus - 1) / kGroupMcus;
-      fg.groups_per_wg = kFusedGroupsPerWg;
-    }
-    if (c->fused) {
-      for (int p = 0; p < 2; p++) {
-        PlaneScale &ps = c->ps[p];
-        if ((rc = dmalloc(&ps.d_fh, ps.fh.size())) || (rc = dmalloc(&ps.d_fv, ps.fv.size()))) return rc;
-        HIP_TRY(hipMemcpy(ps.d_fh, ps.fh.data(), ps.fh.size() * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(ps.d_fv, ps.fv.data(), ps.fv.size() * 4, hipMemcpyHostToDevice));
-      }
-    }
   }
 
-  // persistent k_encode / k_scale_encode grids: every CU filled with as many workgroups as fit
+  // persistent k_encode grid: every CU filled with as many workgroups as fit
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -833,16 +768,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // pulls the units left; sized to its own occupancy it measured 1.8% slower on c1
   // (profiles/r04an_c1_count_grid_tail_prio.txt)
   c->enc_grid_cnt = c->enc_grid;
-  size_t stage_cols = (size_t)c->enc_grid * kWavesPerWg;
-  if (c->fused) {
-    int fper = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &fper, c->optimal ? (const void *)k_scale_encode<8, 5, true, kCount> : (const void *)k_scale_encode<8, 5, true, kEmitDefault>,
-        64 * kFusedWaves, 0));
-    c->fused_grid = std::max(1, ncu * std::max(1, fper));
-    stage_cols = std::max(stage_cols, (size_t)c->fused_grid * kFusedWaves);
-  }
-  c->stage_cols = stage_cols;
+  c->stage_cols = (size_t)c->enc_grid * kWavesPerWg;
   return alloc_slot(c, c->slot[0]);
 }
 
@@ -877,22 +803,6 @@ int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
   return MJG_OK;
 }
 
-template <int HT, int NPV, bool RANGE_ON, int MODE>
-void launch_fused3(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
-  k_scale_encode<HT, NPV, RANGE_ON, MODE><<<c->fused_grid, 64 * kFusedWaves, 0, S.st>>>(
-      src, c->geom, c->fgeom, c->d_tabs, (const uint32_t *)c->ps[0].d_fh, (const uint32_t *)c->ps[0].d_fv,
-      (const uint32_t *)c->ps[1].d_fh, (const uint32_t *)c->ps[1].d_fv, S.d_scratch, S.d_chunk_bits,
-      S.d_stage_bits, S.d_work, n, S.d_hist, S.d_syms, S.d_symn);
-}
-
-template <int MODE>
-void launch_fused(mjg_ctx *c, Slot &S, const uint8_t *src, int n) {
-  const bool range = !c->cfg.in_full_range;
-  if (c->ps[0].g.htaps == 8)
-    range ? launch_fused3<8, 5, true, MODE>(c, S, src, n) : launch_fused3<8, 5, false, MODE>(c, S, src, n);
-  else
-    range ? launch_fused3<4, 3, true, MODE>(c, S, src, n) : launch_fused3<4, 3, false, MODE>(c, S, src, n);
-}
 
 template <int MODE, bool MF, bool DBG>
 void launch_encode3(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
@@ -1013,7 +923,7 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
     }
   }
   SegList enc_in = in_sl;
-  if (c->scale && !c->fused) {
+  if (c->scale) {
     tmark(c, S, MJG_K_SCALE, 0);
     const ScaleGeom &lg = c->ps[0].g, &cg = c->ps[1].g;
     // luma, then U and V in one launch (same filters; blockIdx.z >= n is V) while 2n fits the
@@ -1079,10 +989,7 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
   if (c->optimal) {  // pass 1: symbol counts per frame, then the frame's tables
     tmark(c, S, MJG_K_HUFF, 0);
     HIP_TRY(hipMemsetAsync(S.d_hist, 0, (size_t)n * kFrameTabWords * 4, S.st));
-    if (c->fused)
-      launch_fused<kCount>(c, S, src, n);
-    else
-      launch_encode<kCount>(c, S, enc_in, std::min(wgs, c->enc_grid_cnt), ntasks);
+    launch_encode<kCount>(c, S, enc_in, std::min(wgs, c->enc_grid_cnt), ntasks);
     HIP_TRY(hipMemsetAsync(S.d_work, 0, (size_t)kXcds * kCtrStride * 4, S.st));  // unit counters for pass 2
     k_huff_build<<<n * 4, 64, 0, S.st>>>(S.d_hist, S.d_ftabs, S.d_dht, S.d_dht_nval);
     tmark(c, S, MJG_K_HUFF, 1);
@@ -1093,8 +1000,6 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
     k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, S.st>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
                                                              S.d_scratch, S.d_chunk_bits, S.d_stage_bits,
                                                                   ntasks);
-  else if (c->fused)
-    launch_fused<kEmitDefault>(c, S, src, n);
   else
     launch_encode<kEmitDefault>(c, S, enc_in, wgs, ntasks);
   tmark(c, S, MJG_K_ENCODE, 1);
@@ -1177,7 +1082,7 @@ int launch_held(mjg_ctx *c) {
 // Launch the held jobs when a launch slot is free and they are `merge` jobs (with hold_idle off,
 // also when the GPU has nothing else queued); a lone held job launches at its own mjg_sync (or
 // before a host submit).  Holding even on an idle GPU keeps every launch of a stream of device
-// submits a full pair: A/B with prewarmed clocks (profiles/r05_merge_ab.txt) c5 +6%, c1 +3.5%,
+// submits a full pair: A/B with prewarmed clocks (profiles/r05/merge_prewarm_ab.txt) c5 +6%, c1 +3.5%,
 // c4 +1.5%, c2 +0-1% against no merging; launching a lone job on an idle GPU made the first
 // launch a single and lost that gain on c2.  At mjg_sync the slot of the job just synced stays
 // untouched: its results are read (mjg_fetch, mjg_output_device) until the caller's next submit.
@@ -1220,7 +1125,6 @@ int mjg_max_segments(void) { return kMaxSegs; }
 int mjg_submit_segments(mjg_ctx *c, const uint8_t *const *seg_frames, const int *seg_nframes, int nsegs) {
   if (!c || !seg_frames || !seg_nframes) return set_err(MJG_E_INVALID, "null argument");
   if (nsegs < 1 || nsegs > kMaxSegs) return set_err(MJG_E_INVALID, "nsegs %d not in 1..%d", nsegs, kMaxSegs);
-  if (c->fused) return set_err(MJG_E_INVALID, "multi-segment submits: not with the opt-in fused scale kernel");
   SegList sl;
   int n = 0;
   for (int k = 0; k < kMaxSegs; k++) {
@@ -1278,7 +1182,7 @@ int mjg_sync(mjg_ctx *c, uint64_t *frame_sizes, uint64_t *total) {
       }
       if (c->timing) {
         for (int k = 0; k < MJG_NUM_KERNELS; k++) {
-          if (k == MJG_K_SCALE && (!c->scale || c->fused)) continue;
+          if (k == MJG_K_SCALE && !c->scale) continue;
           if (k == MJG_K_HUFF && !c->optimal) continue;
           const bool tail = k == MJG_K_SCAN_BITS || k == MJG_K_COUNT_FF || k == MJG_K_SCAN_FF || k == MJG_K_WRITE;
           if (tail != c->timing_detail && (tail || k == MJG_K_TAIL)) continue;
@@ -1471,8 +1375,7 @@ int mjg_debug_coefs(mjg_ctx *c, int frame, int16_t *out, size_t nblocks) {
 
 int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   if (!c || !out) return set_err(MJG_E_INVALID, "null argument");
-  if (!c->scale || c->fused)
-    return set_err(MJG_E_STATE, "context does not scale, or scales fused (opened with MJG_F_FUSED)");
+  if (!c->scale) return set_err(MJG_E_STATE, "context does not scale");
   if (pending_jobs(c) > 0) {  // the latest synced submit's planes
     const int rc = mjg_sync(c, nullptr, nullptr);
     if (rc) return rc;

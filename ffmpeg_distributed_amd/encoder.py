@@ -56,7 +56,7 @@ class MjpegEncoder:
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
                  debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
                  huffman: str = "default", chroma: str = "420", rst: bool = False,
-                 fused: bool = False, dct_mfma: Optional[bool] = None, merge: bool = True):
+                 dct_mfma: Optional[bool] = None, merge: bool = True):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -80,8 +80,6 @@ class MjpegEncoder:
             raise ValueError(f"huffman {huffman!r}")
         if rst:
             flags |= _lib.MJG_F_RST
-        if fused:  # -vf scale as one kernel, k_scale_encode (opt-in: slower on MI355X)
-            flags |= _lib.MJG_F_FUSED
         # k_encode's DCT stage: None = the library's choice (matrix cores with -vf scale),
         # True = the matrix cores, False = the VALU passes
         if dct_mfma is True:
@@ -186,7 +184,7 @@ class MjpegEncoder:
     def submit_segments(self, segments):
         """Queue several segments as ONE submit (mjg_submit_segments): `segments` is a list of
         (device_ptr, nframes) on this GPU, at most mjg_max_segments() of them, totalling at
-        most max_batch frames; not with fused=True.  One launch per kernel covers them
+        most max_batch frames.  One launch per kernel covers them
         all; sync() then returns the frames' sizes in segment order and fetch() their JPEGs,
         the same bytes as one submit() per segment.  Every segment's device buffer must stay
         alive until this submit is synced (the kernels read it in place)."""

@@ -61,12 +61,10 @@ extern "C" {
 #define MJG_F_TIMING_DETAIL 64u /* MJG_F_TIMING plus events around every tail kernel (scan, 0xFF
                                   count, write: MJG_K_SCAN_BITS .. MJG_K_WRITE); each event adds
                                   ~10 us of GPU idle between those short kernels */
-#define MJG_F_FUSED 128u       /* with -vf scale: scale and encode in one kernel, k_scale_encode
-                                  (scaled pixels kept in LDS, never in HBM) instead of k_scale
-                                  (scaled frames to HBM) + k_encode.  Same bytes.  Opt-in: on
-                                  MI355X it measures slower than the two kernels (DESIGN.md
-                                  section 3b).  Ignored with MJG_F_DEBUG_COEFS, RST, non-4:2:0 or
-                                  filters it does not handle */
+#define MJG_F_FUSED 128u       /* retired (r05): the one-kernel scale + encode (k_scale_encode)
+                                  measured slower than k_scale + k_encode on MI355X and left the
+                                  library; the flag is accepted and ignored
+                                  (the bytes never depended on it) */
 
 #define MJG_F_DCT_MFMA 256u    /* -huffman default: k_encode's two jfdctint passes on the matrix cores
                                   (v_mfma_f32_32x32x16_f16: pass 1 exact in two f16 digits, pass 2
@@ -79,8 +77,8 @@ extern "C" {
                                   has a launch queued and launched two at a time, see mjg_submit) */
 
 /* Kernel ids for mjg_kernel_times() */
-#define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane; not with MJG_F_FUSED) */
-#define MJG_K_ENCODE 1         /* load [+ fused scale] + FDCT + quant + Huffman -> chunk bits */
+#define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane) */
+#define MJG_K_ENCODE 1         /* load + FDCT + quant + Huffman -> chunk bits */
 #define MJG_K_SCAN_BITS 2      /* per-frame exclusive scan of chunk bit lengths      */
 #define MJG_K_COUNT_FF 3       /* realign chunk bits, pad, count 0xFF per chunk group */
 #define MJG_K_SCAN_FF 4        /* per-frame scan of 0xFF counts -> frame sizes, offsets */
@@ -144,7 +142,7 @@ int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
 int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
 /* Several segments in one submit: segment k's seg_nframes[k] packed I420 frames at device
  * pointer seg_frames[k] (on ctx's device), nsegs in 1..mjg_max_segments(), the total within
- * max_batch; not with MJG_F_FUSED.  One launch of each kernel (k_scale, k_encode, the tail) covers all
+ * max_batch.  One launch of each kernel (k_scale, k_encode, the tail) covers all
  * of them, so the launch's ramp and drain are paid once; the output is the frames in segment
  * order, exactly the bytes of one mjg_submit per segment.  The resident encoder / a GPU worker
  * with several segments queued on one GPU (ffmpeg_distributed.py:139-141 once per segment)
@@ -205,7 +203,7 @@ int mjg_sws_filter(int src_len, int dst_len, int one, int align, int bitexact, i
  * in coding order (4:2:0: Y0 Y1 Y2 Y3 Cb Cr per MCU).  Needs MJG_F_DEBUG_COEFS. */
 int mjg_debug_coefs(mjg_ctx *ctx, int frame, int16_t *out, size_t nblocks);
 /* The full-range encoder-input planes (after scale/range stage) of frame `frame`,
- * packed planar at dst size.  Only for a scaling config on the k_scale path (not MJG_F_FUSED). */
+ * packed planar at dst size.  Only for a scaling config. */
 int mjg_debug_planes(mjg_ctx *ctx, int frame, uint8_t *out, size_t cap);
 /* Filter tables the context generated: plane 0 = luma, 1 = chroma; dir 0 = horizontal,
  * 1 = vertical.  taps/len may be queried with coeff == NULL. */

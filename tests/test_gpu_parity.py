@@ -225,20 +225,19 @@ def test_scale_matches_oracle(sw, sh, dw, dh, full):
         gy, gu, gv = split_i420(planes[i], dw, dh)
         assert (gy == ry).all() and (gu == ru).all() and (gv == rv).all()
     assert got == oracle_frames(frames, sw, sh, q, full, dw, dh)
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, fused=True) as enc:
-        assert enc.encode(frames) == got  # the fused k_scale_encode path (where it applies)
 
 
-FUSED_CASES = [
-    # (sw, sh, dw, dh, q, full, kind, n, huffman): fused k_scale_encode vs the oracle
+SCALE_CASES = [
+    # (sw, sh, dw, dh, q, full, kind, n, huffman): k_scale + k_encode vs the oracle (the cases
+    # of the one-kernel k_scale_encode, retired in r05, kept for the two-kernel path)
     (3840, 2160, 1920, 1080, 3, False, "testsrc", 3, "default"),   # BASELINE configs[3]
     (3840, 2160, 1920, 1080, 3, True, "noise", 2, "default"),
     (3840, 2160, 1920, 1080, 5, False, "testsrc", 2, "optimal"),
     (1920, 1080, 1280, 720, 4, False, "smooth", 2, "default"),      # 1.5:1
     (1280, 720, 640, 360, 2, True, "patches", 3, "default"),
     (640, 360, 1280, 720, 5, False, "testsrc", 2, "default"),       # upscale: 4 taps
-    (400, 300, 200, 150, 6, False, "checker", 3, "optimal"),        # < 32 MCUs per row: unfused
-    (96, 64, 48, 32, 3, True, "noise", 2, "default"),               # (unfused)
+    (400, 300, 200, 150, 6, False, "checker", 3, "optimal"),        # < 32 MCUs per row
+    (96, 64, 48, 32, 3, True, "noise", 2, "default"),
     (1040, 530, 520, 265, 5, False, "smooth", 3, "default"),        # 33 MCUs per row, odd height
     (1030, 520, 515, 260, 4, True, "checker", 2, "optimal"),        # edge MCU column, partial group
     (2200, 1300, 1100, 650, 7, False, "patches", 1, "default"),     # nmcu % 32 != 0
@@ -246,26 +245,21 @@ FUSED_CASES = [
 ]
 
 
-@pytest.mark.parametrize("sw,sh,dw,dh,q,full,kind,n,huffman", FUSED_CASES)
-def test_fused_scale_encode_matches_oracle(sw, sh, dw, dh, q, full, kind, n, huffman):
-    """k_scale_encode (scaled pixels kept in LDS) byte-equal to the oracle's scale_plane +
-    encode_frame, and to the unfused k_scale + k_encode path."""
+@pytest.mark.parametrize("sw,sh,dw,dh,q,full,kind,n,huffman", SCALE_CASES)
+def test_scale_encode_cases_match_oracle(sw, sh, dw, dh, q, full, kind, n, huffman):
+    """k_scale + k_encode byte-equal to the oracle's scale_plane + encode_frame (2:1, 1.5:1,
+    upscale, odd sizes, partial MCU rows, both Huffman modes)."""
     frames = rand_frames(sw, sh, n, seed=sw + dh + q, kind=kind)
-    with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman,
-                      fused=True) as enc:
-        got = enc.encode(frames)
     with MjpegEncoder(0, sw, sh, dw, dh, qscale=q, full_range=full, max_batch=2, huffman=huffman) as enc:
-        got_unfused = enc.encode(frames)
+        got = enc.encode(frames)
     ref = _oracle_many(frames, sw, sh, dst_w=dw, dst_h=dh, full_range=full, qscale=q, huffman=huffman)
     for i in range(n):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
-    assert got_unfused == got
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_scaled_4k_segment_batch_from_device_memory(fused):
+def test_scaled_4k_segment_batch_from_device_memory():
     """BASELINE configs[3] as bench.py submits it: 120 4K frames by device pointer through
-    k_scale + k_encode (and the opt-in fused kernel), every frame equal to the oracle."""
+    k_scale + k_encode, every frame equal to the oracle."""
     import torch
     from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
     w, h, n = 3840, 2160, 120
@@ -275,7 +269,7 @@ def test_scaled_4k_segment_batch_from_device_memory(fused):
         pool[i:i + 20] = testsrc2_i420_torch(w, h, 500 + i, 20, dev)
     torch.cuda.synchronize()
     host = pool.cpu().numpy()
-    with MjpegEncoder(0, w, h, 1920, 1080, qscale=3, max_batch=n, fused=fused) as enc:
+    with MjpegEncoder(0, w, h, 1920, 1080, qscale=3, max_batch=n) as enc:
         enc.submit(device_ptr=pool.data_ptr(), nframes=n)
         got = enc.fetch()
     ref = _oracle_many(host, w, h, dst_w=1920, dst_h=1080, qscale=3)
@@ -440,7 +434,7 @@ def test_submit_segments_scaled_match_oracle(w, h, dw, dh, q):
 
 def test_submit_segments_rejects_bad_lists():
     """Errors, not undefined behaviour: no segments, more than mjg_max_segments(), a total
-    over max_batch, an empty segment, and the opt-in fused scale kernel."""
+    over max_batch and an empty segment."""
     import torch
     from ffmpeg_distributed_amd._lib import MjgError
     w, h = 64, 48
@@ -453,10 +447,6 @@ def test_submit_segments_rejects_bad_lists():
                 enc.submit_segments(bad)
         enc.submit_segments([(t.data_ptr(), 2), (t.data_ptr(), 2)])  # still usable
         assert len(enc.sync()) == 4
-    big = torch.zeros((1, i420_frame_bytes(1280, 720)), dtype=torch.uint8, device="cuda:0")
-    with MjpegEncoder(0, 1280, 720, 640, 360, qscale=5, max_batch=1, fused=True) as enc:  # fusable
-        with pytest.raises(MjgError):
-            enc.submit_segments([(big.data_ptr(), 1)])
 
 
 def test_8k_yuvj420p_matches_oracle():

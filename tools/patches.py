@@ -75,7 +75,7 @@ PATCHES = {
 """)],
     # -huffman optimal counting pass without its LDS histogram atomics / without its symbol
     # record stores (timing probes: wrong tables / wrong replay; c1: 0.753 -> 0.658 / 0.817 ms,
-    # profiles/r05_c1_count_ablation.txt).  Counting the DC and EOB symbols per distinct value
+    # profiles/r05/c1_count_ablation.txt).  Counting the DC and EOB symbols per distinct value
     # after the block (a ballot loop) instead of per lane measured slower: 0.791 vs 0.760 ms.
     "cnt_noatomic": lambda a: [(K, "    atomicAdd(&hdc[cat], 1u);\n", ""), (K, "    atomicAdd(&hac[sym], 1u);\n", "")],
     "cnt_norec": lambda a: [(K, "    rec[n * 64] = (1u << 31) | ((uint32_t)cat << 16) | mant;\n", ""),

@@ -19,7 +19,6 @@ from pmc_summary import load, load_totals  # noqa: E402
 # dominant (read, write) access width of each kernel, bytes per lane
 KERNEL_WIDTH = {
     "k_encode": (8, 4),       # 8-byte pixel row loads, slot words
-    "k_fused": (4, 4),        # 4-byte window loads (scale + encode), slot words
     "k_scale": (8, 1),        # 16-byte window loads (4 and 8 B reads calibrate alike), byte stores
     "k_emit_syms": (4, 4),    # symbol record words, slot words
     "k_count_ff": (4, 4),     # slot words

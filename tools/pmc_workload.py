@@ -15,7 +15,6 @@ def main():
     p.add_argument("--workload", default="c2")
     p.add_argument("--content", default="testsrc")
     p.add_argument("--launches", type=int, default=3)
-    p.add_argument("--fused", action="store_true", help="-vf scale as the fused k_scale_encode")
     p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto", help="k_encode's DCT stage")
     a = p.parse_args()
     import torch
@@ -32,7 +31,7 @@ def main():
         pool[i:i + k] = gen(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
     enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF,
-                       fused=a.fused, dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
+                       dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
     tot = 0
     for _ in range(a.launches):
         enc.submit(device_ptr=pool.data_ptr(), nframes=SEG)

@@ -45,7 +45,7 @@ def union(iv):
 
 
 def is_encode(name):
-    return "k_encode" in name or "k_scale_encode" in name or "k_emit_syms" in name
+    return "k_encode" in name or "k_emit_syms" in name
 
 
 def main():
@@ -56,10 +56,9 @@ def main():
         sys.exit(f"{sys.argv[1]}: {len(marks)} marker kernels (spin_kernel); need bench.py's trace markers")
     t0, t1 = marks[0][1], marks[1][0]
     region = [r for r in rows if t0 <= r[0] and r[1] <= t1 and "mjg" in r[2]]
-    # the last stage of a launch's encode: k_emit_syms (-huffman optimal) / k_encode / fused
+    # the last stage of a launch's encode: k_emit_syms (-huffman optimal) / k_encode
     last_stage = "k_emit_syms" if any("k_emit_syms" in r[2] for r in region) else None
     enc = [r for r in region if (last_stage in r[2] if last_stage else is_encode(r[2]))]
-    first = [r for r in region if "k_scale" in r[2] or ("k_encode" in r[2] and last_stage)]  # launch starts
     starts = [r[0] for r in enc]
     n = len(enc)
     f = lambda v: (f"median {st.median(v):9.1f}  min {min(v):9.1f}  max {max(v):9.1f} us" if v else "n/a")
