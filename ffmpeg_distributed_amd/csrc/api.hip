@@ -942,8 +942,14 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
           sg.d_poff = (long long)g.cw * g.ch;
         }
       }
-      dim3 grid = ps.grid;
-      grid.z = p && uv1 ? 2 * n : n;
+      // one dimension: tiles x planes x frames (scale.hip decodes it by multiply-high)
+      const int nz = p && uv1 ? 2 * n : n;
+      sg.gx = (int)ps.grid.x;
+      sg.gxy = (int)(ps.grid.x * ps.grid.y);
+      auto magic = [](uint32_t d) { return d > 1 ? (uint32_t)((((uint64_t)1 << 32) + d - 1) / d) : 0u; };
+      sg.gx_magic = magic((uint32_t)sg.gx);
+      sg.gxy_magic = magic((uint32_t)sg.gxy);
+      const dim3 grid((unsigned)(sg.gxy * nz), 1, 1);
 #define MJG_SCALE_LAUNCH3(HT, NPV, D4, TH)                                                          \
   do {                                                                                              \
     if (sg.range == 1)                                                                              \

@@ -58,7 +58,19 @@ struct ScaleGeom {
   int lds_pairs;                 // max row pairs any tile needs
   int lds_win_words;             // max source-window dwords any tile needs (TH 64: rows at
                                  // kScaleAliasWords, the pair image inside it)
+  // the launch is a 1-D grid of gx * gy * (planes x frames) tiles; tile t -> (bx, by, z) by
+  // multiply-high with ceil(2^32 / d), not by two scalar divisions (div_magic)
+  int gx, gxy;
+  uint32_t gx_magic, gxy_magic;  // 0 when the divisor is 1
 };
+
+// t / d for 0 <= t < 2^31: with m = ceil(2^32 / d), umulhi(t, m) is t / d or one more (the
+// error t (m - 2^32/d) / 2^32 < 1), corrected by one compare; d = 1: m = 0
+__device__ __forceinline__ int div_magic(int t, uint32_t magic, int d) {
+  if (!magic) return t;
+  const int q = (int)__umulhi((uint32_t)t, magic);
+  return q * d > t ? q - 1 : q;
+}
 
 __device__ __forceinline__ int sws_range(int v, int range) {
   if (range == 1) {  // |v| < 2^15: the 24-bit multiply is exact
@@ -123,19 +135,16 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const SegList sr
   static_assert(!ALIAS || (HT == 8 && NPV == 5), "64/128-row tiles: 2:1 filters only");
   // wave index as a uniform value: the v-pass rows (and their filter rows) are wave-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int bx = blockIdx.x, by = blockIdx.y, z = blockIdx.z;
+  int t = blockIdx.x;  // the tile, raster order within a (plane, frame), then z
   if (ALIAS) {
     // XCD-contiguous tile order: workgroup i runs on XCD i % 8 (round-robin dispatch), so XCD
     // j takes the j-th eighth of the tiles in raster order and horizontally adjacent tiles --
     // whose windows share the 128-byte lines at their edges -- meet in the same L2
-    const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
-    const int i = bx + gx * (by + gy * z), j = i & 7, q = n >> 3, r = n & 7;
-    const int t = j * q + min(j, r) + (i >> 3);
-    z = t / (gx * gy);
-    const int rem = t - z * gx * gy;
-    by = rem / gx;
-    bx = rem - by * gx;
+    const int i = t, n = gridDim.x, j = i & 7, q = n >> 3, r = n & 7;
+    t = j * q + min(j, r) + (i >> 3);
   }
+  const int z = div_magic(t, g.gxy_magic, g.gxy), rem = t - z * g.gxy;
+  const int by = div_magic(rem, g.gx_magic, g.gx), bx = rem - by * g.gx;
   const int x0 = bx * kScaleTileW, y0 = by * TH;
   const int pl = z >= g.nf, f = z - (pl ? g.nf : 0);
   const uint8_t *s = seg_frame(src, f, g.s_fstride) + g.s_off + (pl ? g.s_poff : 0);
