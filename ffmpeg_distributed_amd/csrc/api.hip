@@ -177,6 +177,12 @@ constexpr int kSlots = 2;
 // so the launch's ramp and drain (T(n) = 0.115 ms + 4.48 us n per 4K launch) is
 // paid once per kMerge submits.  Each submit stays a job of its own for mjg_sync / mjg_fetch.
 constexpr int kMerge = 2;
+// k_emit_syms workgroups per k_encode workgroup: the replay waits on its record loads most of
+// its time (SQ_WAIT_ANY 72% of its wave cycles, profiles/r05/head_sq_c1.json) and needs 54
+// VGPRs and 8.7 KB of LDS, so more waves per SIMD than k_encode's four hide that latency.
+// bench c1 (profiles/r05/c1_emit_grid_bench.txt): x1 390-396K fps, x2 410-415K, x4 418-421K,
+// x8 405-418K; k_emit_syms alone 0.258 / 0.261 / 0.210 / 0.190 ms per 250 1080p frames
+constexpr int kEmitGridMul = 4;
 // merging is off when the slots' doubled scratch would take more than this share of the
 // device's free memory (slot buffers scale with the frames a launch may carry)
 constexpr double kMergeMemShare = 0.25;
@@ -768,7 +774,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   // pulls the units left; sized to its own occupancy it measured 1.8% slower on c1
   // (profiles/r04an_c1_count_grid_tail_prio.txt)
   c->enc_grid_cnt = c->enc_grid;
-  c->stage_cols = (size_t)c->enc_grid * kWavesPerWg;
+  c->stage_cols = (size_t)c->enc_grid * kWavesPerWg * (c->optimal ? kEmitGridMul : 1);
   return alloc_slot(c, c->slot[0]);
 }
 
@@ -1003,7 +1009,7 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
   }
   tmark(c, S, MJG_K_ENCODE, 0);
   if (c->optimal)
-    k_emit_syms<<<c->enc_grid, 64 * kWavesPerWg, 0, S.st>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
+    k_emit_syms<<<c->enc_grid * kEmitGridMul, 64 * kWavesPerWg, 0, S.st>>>(g, c->d_tabs, S.d_ftabs, S.d_syms, S.d_symn,
                                                              S.d_scratch, S.d_chunk_bits, S.d_stage_bits,
                                                                   ntasks);
   else
