@@ -27,6 +27,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -348,6 +349,30 @@ def e2e(workload: str, device: int, segments: int, tmpdir=None):
             r = leg(per_process(True), segments)
             r["argv"] = "mjg_client --device N -- <remote_args> (resident encoder per GPU)"
             out["per_segment_process"] = r
+            # two -H gpu:N entries for one GPU (fd.py: two TaskThreads, fd.py:185-192): two
+            # per-segment processes at a time, so one segment's host read and H2D overlap the
+            # other's (one segment at a time is bound by its own 1.49 GB crossing PCIe)
+            one = per_process(True)
+            errs = []
+
+            def client(j):
+                for i in range(segments):
+                    rc = one(os.path.join(d, f"out_c{j}_{i}.mkv"))
+                    if rc != 0:
+                        errs.append(rc)
+            ths = [threading.Thread(target=client, args=(j,)) for j in range(2)]
+            t0 = time.monotonic()
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            wall = time.monotonic() - t0
+            if errs:
+                raise RuntimeError(f"concurrent e2e segments exited {errs}")
+            out["per_segment_process_2clients"] = {
+                "clients": 2, "segments": 2 * segments, "seconds": round(wall, 4),
+                "fps": round(2 * segments * seg_frames / wall, 1),
+                "argv": "two mjg_client processes at a time on one GPU (-H gpu:N given twice)"}
             from ffmpeg_distributed_amd import resident
             if not resident.shutdown(D.CLIENT, device):
                 r["warning"] = "resident encoder still running after its shutdown"
