@@ -80,7 +80,7 @@ def parse():
                    help="also time K = 2, 4 segments per submit (mjg_submit_segments, N=1 only); off by "
                         "default so a profile of the default command holds only the headline's launches")
     p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
-                   help="-huffman default: k_encode's DCT stage (auto: the matrix cores with -vf scale)")
+                   help="-huffman default: k_encode's DCT stage (auto: the VALU passes; mfma: the matrix cores)")
     p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
     p.add_argument("--kernel-timing-detail", action="store_true",
                    help="events around every tail kernel too (adds ~10 us idle per event)")
@@ -691,7 +691,7 @@ def main():
                        **({"scale_kernels": "k_scale + k_encode"}
                           if (DW, DH) != (W, H) else {}),
                        "dct": "VALU (k_encode<.., optimal counting pass>)" if HUFF == "optimal" else
-                              ("matrix cores (dct_mfma)" if a.dct == "mfma" or (a.dct == "auto" and (DW, DH) != (W, H))
+                              ("matrix cores (dct_mfma)" if a.dct == "mfma"
                                else "VALU (row_pass + column_screen)")},
             "roofline": primary,
             "roofline_kernels": per_kernel,

@@ -628,10 +628,11 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
                         c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
-  // -huffman default: MFMA when the encode input is k_scale's output (measured faster there,
-  // DESIGN.md section 4c), or forced either way by the flags
-  c->dct_mfma = !c->optimal && !(k.flags & MJG_F_DCT_VALU) &&
-                ((k.flags & MJG_F_DCT_MFMA) || c->scale);
+  // -huffman default: the DCT stage on the matrix cores only when MJG_F_DCT_MFMA asks for it.
+  // It was the default with -vf scale until r05; since the VALU passes' round-4 changes the VALU
+  // stage is as fast or faster there too (bench c4 155.0K vs 154.0K fps, natural +1.8%,
+  // noise-patches +13%: profiles/r05/c4_dct_stage_ab.txt)
+  c->dct_mfma = !c->optimal && !(k.flags & MJG_F_DCT_VALU) && (k.flags & MJG_F_DCT_MFMA);
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),

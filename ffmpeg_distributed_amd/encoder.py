@@ -80,7 +80,7 @@ class MjpegEncoder:
             raise ValueError(f"huffman {huffman!r}")
         if rst:
             flags |= _lib.MJG_F_RST
-        # k_encode's DCT stage: None = the library's choice (matrix cores with -vf scale),
+        # k_encode's DCT stage: None = the library's choice (the VALU passes),
         # True = the matrix cores, False = the VALU passes
         if dct_mfma is True:
             flags |= _lib.MJG_F_DCT_MFMA

@@ -68,10 +68,10 @@ extern "C" {
 
 #define MJG_F_DCT_MFMA 256u    /* -huffman default: k_encode's two jfdctint passes on the matrix cores
                                   (v_mfma_f32_32x32x16_f16: pass 1 exact in two f16 digits, pass 2
-                                  a quantiser screen), dct_mfma in kernels.hip.  Same bytes.  The
-                                  default with -vf scale (measured faster there); this flag forces
-                                  it for unscaled input */
-#define MJG_F_DCT_VALU 512u    /* -huffman default: the VALU passes even with -vf scale (A/B) */
+                                  a quantiser screen), dct_mfma in kernels.hip.  Same bytes.  Opt-in
+                                  (the default with -vf scale until r05, now measured slower or
+                                  equal there too: DESIGN.md section 4.3) */
+#define MJG_F_DCT_VALU 512u    /* -huffman default: the VALU passes (the default; overrides DCT_MFMA) */
 #define MJG_F_NO_MERGE 1024u   /* no library-side merging: every mjg_submit is a launch of its own
                                   (by default single-segment device submits are held while the GPU
                                   has a launch queued and launched two at a time, see mjg_submit) */
