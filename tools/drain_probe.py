@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """k_encode's per-launch fixed cost (its drain and launch ramp) from synced launches of 60 /
-120 / 240 / 480 4K frames: T(n) = a + b n.  usage (GPU box): python3 tools/drain_probe.py"""
+120 / 240 / 480 4K frames: T(n) = a + b n, after a 1 s prewarm, sizes interleaved over ROUNDS.
+usage (GPU box): [WL=c2] [CONTENT=testsrc] python3 tools/drain_probe.py"""
 import os
 import sys
 
@@ -23,17 +24,27 @@ def main():
         pool[i:i + 20] = CONTENT[content](W, H, i % 120, 20, dev, full_range=FULL)
     torch.cuda.synchronize()
     enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=nmax, timing=True, huffman=HUFF)
-    ns, ts = [60, 120, 240, 480], []
-    for n in ns:
-        enc.submit(device_ptr=pool.data_ptr(), nframes=n)
+    import time
+    ns = [60, 120, 240, 480]
+    # prewarm: the GPU leaves its idle clocks only after ~0.3 s of load (bench.py --prewarm-ms)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < float(os.environ.get("PREWARM_S", "1.0")):
+        enc.submit(device_ptr=pool.data_ptr(), nframes=120)
         enc.sync()
-        enc.kernel_times(reset=True)
-        for _ in range(5):
-            enc.submit(device_ptr=pool.data_ptr(), nframes=n)
-            enc.sync()
-        kt, nl = enc.kernel_times()
-        ts.append(kt["encode"])
-        print(f"{content} n={n}: k_encode {kt['encode']:.4f} ms ({kt['encode'] / n * 1e3:.2f} us/frame)", flush=True)
+    res = {n: [] for n in ns}
+    for rnd in range(int(os.environ.get("ROUNDS", "3"))):  # sizes interleaved, not one block each
+        for n in ns:
+            enc.kernel_times(reset=True)
+            for _ in range(5):
+                enc.submit(device_ptr=pool.data_ptr(), nframes=n)
+                enc.sync()
+            kt, nl = enc.kernel_times()
+            res[n].append(kt["encode"])
+    ts = []
+    for n in ns:
+        t = sorted(res[n])[len(res[n]) // 2]
+        ts.append(t)
+        print(f"{content} n={n}: k_encode median {t:.4f} ms ({t / n * 1e3:.2f} us/frame), rounds {[round(x, 4) for x in res[n]]}", flush=True)
     b, a = np.polyfit(ns, ts, 1)
     print(f"fit T(n) = {a:.4f} ms + {b * 1e3:.3f} us x n: fixed part at n=120 = {a / (a + b * 120) * 100:.1f}%")
     enc.close()

@@ -20,6 +20,7 @@ for c in natural noise-patches; do
   timeout -k 10 300 python bench.py --content $c --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_c2_$c.json 2> $O/bench_c2_$c.err || exit 1
 done
 timeout -k 10 900 bash tools/pmc_traffic.sh > $O/pmc_traffic.log 2>&1 || { tail -5 $O/pmc_traffic.log; exit 1; }
+cp profiles/pmc_c*.json $O/  # pmc_traffic.py writes profiles/ on the box: bring the files back
 SQ="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY"
 SQ2="SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_BRANCH"
 for w in c2 c1 c4; do
