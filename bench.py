@@ -586,6 +586,11 @@ def main():
         bytes_out.clear()
         trace_marker()
 
+    # The marker kernel's first launch loads its code object (~2.6 ms on the host, measured in
+    # the r05 HEAD trace): done here, not in the idle gap right before the timed steps, where the
+    # GPU would drop its clock (a 2 ms idle gap before 20 steps costs 7%: tools/region_probe.py,
+    # profiles/r05/region_probe.txt)
+    trace_marker()
     prewarm = 0
     if a.prewarm_ms > 0:
         t_pw = time.perf_counter()

@@ -3,7 +3,8 @@
 --kernel-trace --output-format csv -- python3 bench.py ...`).
 
 bench.py brackets its timed steps with a tiny marker kernel on torch's stream (`trace_marker`:
-torch.cuda._sleep, "spin_kernel" in the trace): the first marker runs after the warmup drain,
+torch.cuda._sleep, "spin_kernel" in the trace; bench.py also launches one at set-up, before the
+prewarm, which is skipped here: the last three are used): the first runs after the warmup drain,
 the second after the timed steps' final sync, the third after the isolated launches.  So the
 k_encode dispatches between markers 1 and 2 are exactly the timed region's launches, and those
 between markers 2 and 3 the isolated ones (4 of one segment, then 4 of two segments, each
@@ -52,6 +53,8 @@ def main():
     rows = load(sys.argv[1])
     bench = json.load(open(sys.argv[2])) if len(sys.argv) > 2 else None
     marks = [r for r in rows if "spin" in r[2] or "sleep" in r[2]]
+    if len(marks) > 3:  # bench.py r05+: a first marker at set-up (loads its code object early)
+        marks = marks[-3:]
     if len(marks) < 2:
         sys.exit(f"{sys.argv[1]}: {len(marks)} marker kernels (spin_kernel); need bench.py's trace markers")
     t0, t1 = marks[0][1], marks[1][0]
