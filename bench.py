@@ -591,6 +591,9 @@ def main():
     # GPU would drop its clock (a 2 ms idle gap before 20 steps costs 7%: tools/region_probe.py,
     # profiles/r05/region_probe.txt)
     trace_marker()
+    # ranks start the prewarm together, so none idles long at the barrier before the timed steps
+    # (an idle GPU drops its clock within milliseconds)
+    barrier()
     prewarm = 0
     if a.prewarm_ms > 0:
         t_pw = time.perf_counter()
