@@ -38,9 +38,13 @@ DECODE_ARGV = ["ffmpeg", "-v", "error", "-f", "matroska", "-i", "pipe:", "-map",
 # large part of its start-up: 4K batches of 32 frames pinned 1.2 GB, of 8 frames 0.3 GB.
 BATCH = int(os.environ.get("MJG_WORKER_BATCH", "0"))
 BATCH_BYTES = int(os.environ.get("MJG_WORKER_BATCH_BYTES", str(96 << 20)))
-# serve mode pins its batches once for many segments: larger batches (an 8K batch of 1 frame
-# leaves the GPU waiting on every sync)
-SERVE_BATCH_BYTES = int(os.environ.get("MJG_SERVE_BATCH_BYTES", str(256 << 20)))
+# serve mode (and the resident encoder) pins its batches once for many segments.  128 MiB (10 4K
+# frames) measured ahead of 256 MiB end to end: a segment's first H2D starts after a smaller
+# first read and its last batch drains sooner (per-segment process 3,490-3,649 vs 3,304-3,392 4K
+# fps, two clients 3,755-3,790 vs 3,289-3,466; profiles/r05/e2e_batch_ab.txt); every batch holds
+# at least 4 frames (an 8K batch of 1 frame leaves the GPU waiting on every sync)
+SERVE_BATCH_BYTES = int(os.environ.get("MJG_SERVE_BATCH_BYTES", str(128 << 20)))
+MIN_BATCH_FRAMES = 4
 # FFmpeg builds differ in the pix_fmt their CLI hands the mjpeg encoder for yuv420p input
 # (yuvj420p: no COM; yuv420p + full range: COM "CS=ITU601"); default = yuvj420p.
 COM_ITU601 = os.environ.get("MJG_COM_ITU601", "0") == "1"
@@ -448,7 +452,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     bind_numa(device)  # before the reader threads and the batch buffers
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
-    batch = opts.batch or max(1, min(32, opts.batch_bytes // max(info.frame_bytes, 1)))
+    batch = opts.batch or max(MIN_BATCH_FRAMES, min(32, opts.batch_bytes // max(info.frame_bytes, 1)))
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     key = (info.width, info.height, dst_w, dst_h, info.full_range, prof.qscale, sar,
