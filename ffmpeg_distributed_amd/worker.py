@@ -45,6 +45,12 @@ BATCH_BYTES = int(os.environ.get("MJG_WORKER_BATCH_BYTES", str(96 << 20)))
 # at least 4 frames (an 8K batch of 1 frame leaves the GPU waiting on every sync)
 SERVE_BATCH_BYTES = int(os.environ.get("MJG_SERVE_BATCH_BYTES", str(128 << 20)))
 MIN_BATCH_FRAMES = 4
+
+
+def batch_frames(opts, frame_bytes: int) -> int:
+    """Frames per page-locked batch: MJG_WORKER_BATCH if set, else what batch_bytes holds,
+    clamped to [MIN_BATCH_FRAMES, 32]."""
+    return opts.batch or max(MIN_BATCH_FRAMES, min(32, opts.batch_bytes // max(frame_bytes, 1)))
 # FFmpeg builds differ in the pix_fmt their CLI hands the mjpeg encoder for yuv420p input
 # (yuvj420p: no COM; yuv420p + full range: COM "CS=ITU601"); default = yuvj420p.
 COM_ITU601 = os.environ.get("MJG_COM_ITU601", "0") == "1"
@@ -452,7 +458,7 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
     bind_numa(device)  # before the reader threads and the batch buffers
     from .encoder import MjpegEncoder, PinnedBuffer   # GPU work starts here
 
-    batch = opts.batch or max(MIN_BATCH_FRAMES, min(32, opts.batch_bytes // max(info.frame_bytes, 1)))
+    batch = batch_frames(opts, info.frame_bytes)
 
     sar = profile.scaled_sar(info.sar, (info.width, info.height), (dst_w, dst_h))
     key = (info.width, info.height, dst_w, dst_h, info.full_range, prof.qscale, sar,

@@ -52,6 +52,18 @@ def test_options_from_request_env():
     assert worker.Options.from_env({}) == worker.Options()
 
 
+def test_batch_frames():
+    """Page-locked batch sizing (r05): the resident encoder's 128 MiB default holds 10 4K
+    frames; an 8K batch never drops below MIN_BATCH_FRAMES; MJG_WORKER_BATCH wins."""
+    from ffmpeg_distributed_amd import worker
+    o = worker.Options.from_env({}, worker.SERVE_BATCH_BYTES)
+    assert worker.SERVE_BATCH_BYTES == 128 << 20
+    assert worker.batch_frames(o, 3840 * 2160 * 3 // 2) == 10
+    assert worker.batch_frames(o, 7680 * 4320 * 3 // 2) == worker.MIN_BATCH_FRAMES == 4
+    assert worker.batch_frames(o, 64 * 64 * 3 // 2) == 32
+    assert worker.batch_frames(worker.Options.from_env({"MJG_WORKER_BATCH": "3"}), 3840 * 2160 * 3 // 2) == 3
+
+
 def fake_run(dev, args, stdin, stdout, stderr, cache, opts):
     """Stands in for worker.run: the segment's bytes, prefixed, with ffmpeg-style progress."""
     data = stdin.read()
