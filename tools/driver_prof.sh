@@ -25,6 +25,8 @@ f=$(find $O/prof -name "*kernel_stats.csv" | head -n 1)
 t=$(find $O/prof -name "*kernel_trace.csv" | head -n 1)
 cp "$f" $O/kernel_stats.csv && cp "$t" $O/kernel_trace.csv && rm -rf $O/prof
 python3 tools/timeline.py $O/kernel_trace.csv $O/prof_bench.json > $O/timeline.txt 2>&1
+# keep the trace small enough to come back (gpurun merges <= 64 MiB): the header, mjg kernels, markers
+{ head -n 1 $O/kernel_trace.csv; grep -E "mjg::|spin_kernel" $O/kernel_trace.csv; } > $O/kernel_trace.small.csv && mv $O/kernel_trace.small.csv $O/kernel_trace.csv
 cat $O/timeline.txt
 grep -E "mjg" $O/kernel_stats.csv | cut -d, -f1-4 | cut -c1-140
 echo done
