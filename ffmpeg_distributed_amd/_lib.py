@@ -44,7 +44,7 @@ EXPORTS = (
     "mjg_frame_bytes", "mjg_header", "mjg_submit", "mjg_sync", "mjg_fetch", "mjg_fetch_host",
     "mjg_output_device", "mjg_stream", "mjg_queue_depth", "mjg_ctx_queue_depth", "mjg_submit_segments", "mjg_max_segments", "mjg_host_alloc", "mjg_host_free",
     "mjg_kernel_times", "mjg_build_header", "mjg_sws_filter", "mjg_debug_coefs",
-    "mjg_debug_planes", "mjg_debug_filter",
+    "mjg_debug_planes", "mjg_debug_filter", "mjg_debug_huff_build",
 )
 
 
@@ -114,13 +114,16 @@ def load():
         L.mjg_debug_planes.argtypes = [vp, C.c_int, u8p, sz]
         L.mjg_debug_filter.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int16),
                                        C.POINTER(C.c_int32), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        if hasattr(L, "mjg_debug_huff_build"):  # absent from libraries built before r05 (A/B builds)
+            L.mjg_debug_huff_build.argtypes = [C.c_int, C.POINTER(C.c_uint32), C.c_int, u8p, C.POINTER(C.c_uint32)]
         L.mjg_build_header.argtypes = [C.POINTER(MjgConfig), u8p, sz, C.POINTER(sz)]
         L.mjg_sws_filter.argtypes = [C.c_int] * 7 + [C.POINTER(C.c_int16), sz, C.POINTER(C.c_int32),
                                                      C.POINTER(C.c_int)]
         # fail loudly on a stale / partial build (an A/B library from before r04/r05 named by
         # MJG_LIBRARY may lack mjg_queue_depth / mjg_ctx_queue_depth: the queue is then two
         # deep, no merging; and the multi-segment submit, which encoder.submit_segments guards)
-        late = (("mjg_queue_depth", "mjg_ctx_queue_depth", "mjg_submit_segments", "mjg_max_segments")
+        late = (("mjg_queue_depth", "mjg_ctx_queue_depth", "mjg_submit_segments", "mjg_max_segments",
+                 "mjg_debug_huff_build")
                 if os.environ.get("MJG_LIBRARY") else ())
         for name in EXPORTS:
             if name not in late:

@@ -1402,6 +1402,34 @@ int mjg_debug_planes(mjg_ctx *c, int frame, uint8_t *out, size_t cap) {
   return MJG_OK;
 }
 
+int mjg_debug_huff_build(int device, const uint32_t *hist, int nframes, uint8_t *dht, uint32_t *nval) {
+  if (!hist || !dht || !nval || nframes < 1 || nframes > 4096) return set_err(MJG_E_INVALID, "bad arguments");
+  HIP_TRY(hipSetDevice(device));
+  const size_t nh = (size_t)nframes * kFrameTabWords, nd = (size_t)nframes * 4 * kDhtSlot, nv = (size_t)nframes * 4;
+  uint32_t *d_hist = nullptr, *d_ftabs = nullptr, *d_nval = nullptr;
+  uint8_t *d_dht = nullptr;
+  int rc = MJG_OK;
+  if (hipMalloc((void **)&d_hist, nh * 4) != hipSuccess || hipMalloc((void **)&d_ftabs, nh * 4) != hipSuccess ||
+      hipMalloc((void **)&d_dht, nd) != hipSuccess || hipMalloc((void **)&d_nval, nv * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    rc = set_err(MJG_E_NOMEM, "hipMalloc failed");
+  }
+  if (rc == MJG_OK && (hipMemcpy(d_hist, hist, nh * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                       hipMemset(d_dht, 0, nd) != hipSuccess)) rc = set_err(MJG_E_HIP, "copy in failed");
+  if (rc == MJG_OK) {
+    k_huff_build<<<nframes * 4, 64>>>(d_hist, d_ftabs, d_dht, d_nval);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(dht, d_dht, nd, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(nval, d_nval, nv * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = set_err(MJG_E_HIP, "k_huff_build failed");
+  }
+  (void)hipFree(d_hist);
+  (void)hipFree(d_ftabs);
+  (void)hipFree(d_dht);
+  (void)hipFree(d_nval);
+  return rc;
+}
+
 int mjg_debug_filter(mjg_ctx *c, int plane, int dir, int16_t *coeff, int32_t *pos, int *taps,
                      int *len) {
   if (!c) return set_err(MJG_E_INVALID, "null ctx");

@@ -209,6 +209,12 @@ int mjg_debug_planes(mjg_ctx *ctx, int frame, uint8_t *out, size_t cap);
  * 1 = vertical.  taps/len may be queried with coeff == NULL. */
 int mjg_debug_filter(mjg_ctx *ctx, int plane, int dir, int16_t *coeff, int32_t *pos,
                      int *taps, int *len);
+/* -huffman optimal's table builder (k_huff_build) on given symbol counts, on GPU `device`:
+ * hist[f][544] (AC luma 0-255, AC chroma 256-511, DC luma 512-527, DC chroma 528-543) for
+ * nframes frames -> dht[f][t][272] (BITS[1..16] then HUFFVAL; t: 0 DC luma, 1 DC chroma,
+ * 2 AC luma, 3 AC chroma) and nval[f][t] (HUFFVAL entries).  Replaces the table build of
+ * ff_mjpeg_encode_huffman_close (libavcodec/mjpegenc_huffman.c); tests compare it with the oracle. */
+int mjg_debug_huff_build(int device, const uint32_t *hist, int nframes, uint8_t *dht, uint32_t *nval);
 
 #ifdef __cplusplus
 }

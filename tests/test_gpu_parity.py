@@ -881,3 +881,44 @@ def test_dct_mfma_4k_segment_from_device_memory():
     ref = _oracle_many(host, w, h, qscale=5)
     for i in range(n):
         assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
+
+
+# ------------------------------------------- k_huff_build on given counts (mjg_debug_huff_build)
+def test_huff_build_matches_oracle_tables():
+    """-huffman optimal's table builder alone, on the 153 count vectors the CPU tests pin the
+    oracle with (random, tie-heavy, 16-bit-limit-forcing, edge cases; those summing past int range
+    scaled down): every frame's four
+    BITS/HUFFVAL equal oracle.huff_optimal (ff_mjpeg_encode_huffman_close: AV_QSORT's tie order
+    decides which equal-count symbols get the longer codes)."""
+    import ctypes as C
+    from ffmpeg_distributed_amd import _lib
+    from test_huffman_optimal import count_vectors
+    L = _lib.load()
+    cv = []
+    for c in count_vectors():
+        # FFmpeg sums counts as int in package weights (<= 16 x the total): a frame's counts
+        # (<= its blocks x 64, 8.3M per 4K table) keep them below 2**31; the geometric vectors
+        # that would not are scaled into that domain.
+        while 16 * int(c.sum()) >= 2 ** 31:
+            c = np.where(c > 0, np.maximum(c >> 4, 1), 0)
+        cv.append(c)
+    n = len(cv)
+    hist = np.zeros((n, 544), np.uint32)
+    for i in range(n):
+        hist[i, 0:256] = cv[i]                      # AC luma
+        hist[i, 256:512] = cv[(i + 1) % n]          # AC chroma
+        hist[i, 512:528] = cv[(i + 2) % n][:16]     # DC luma
+        hist[i, 528:544] = cv[(i + 3) % n][16:32]   # DC chroma
+    dht = np.zeros((n, 4, 272), np.uint8)
+    nval = np.zeros((n, 4), np.uint32)
+    rc = L.mjg_debug_huff_build(0, hist.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                                dht.ctypes.data_as(C.POINTER(C.c_uint8)), nval.ctypes.data_as(C.POINTER(C.c_uint32)))
+    assert rc == 0, L.mjg_last_error()
+    for i in range(n):
+        for t, sl in ((0, slice(512, 528)), (1, slice(528, 544)), (2, slice(0, 256)), (3, slice(256, 512))):
+            c = np.zeros(256, np.uint32)
+            c[:sl.stop - sl.start] = hist[i, sl]
+            bits, vals = oracle.huff_optimal(c)
+            k = int(nval[i, t])
+            assert list(dht[i, t, :16]) == list(bits[1:17]), (i, t)
+            assert k == len(vals) and list(dht[i, t, 16:16 + k]) == list(vals), (i, t)
