@@ -504,24 +504,31 @@ __device__ __forceinline__ uint64_t wave_parallel_blocks(int ncand) {
   return best;
 }
 
-// -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram
-// (layout of the table block: AC luma 0-255, AC chroma 256-511, DC luma 512-527,
-// DC chroma 528-543), mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.
+// -huffman optimal, first pass: count the block's symbols into the wave's LDS histogram,
+// mjpegenc.c record_block / ff_mjpeg_encode_huffman_increment.  The histogram is 16-bit
+// counters in pairs (kCountWords words: AC table t symbol s at word t*128 + (s & 127), half
+// s >> 7; DC table t category c at word 256 + t*8 + (c & 7), half c >> 3: the rare symbols
+// share a word with the common ones, so same-address atomics stay those of one symbol), so
+// that the counting pass fits 4 workgroups per CU; flushed into the frame's 32-bit table block
+// (AC luma 0-255, AC chroma 256-511, DC luma 512-527, DC chroma 528-543) at every frame change
+// and at least every kCountFlush chunks (a symbol occurs at most 63 times per block:
+// 16 x 64 x 63 < 2^16).
 // It also records every symbol with its mantissa in the lane's record column (rec[j * 64]:
 // DC flag << 31 | (DC category or AC symbol) << 16 | mantissa), so the emission pass
 // replays the symbols (k_emit_syms) instead of recomputing the block.
 constexpr int kSymCap = 68;  // symbols per block: DC + 63 AC + 3 ZRL + EOB
+constexpr int kCountWords = 272, kCountFlush = 16;
 struct CountSink {
   uint32_t *hac, *hdc;
   uint32_t *rec;
   uint32_t n = 0;
   __device__ __forceinline__ void dc(int cat, uint32_t mant) {
-    atomicAdd(&hdc[cat], 1u);
+    atomicAdd(&hdc[cat & 7], 1u << ((cat >> 3) << 4));
     rec[n * 64] = (1u << 31) | ((uint32_t)cat << 16) | mant;
     n++;
   }
   __device__ __forceinline__ void ac(int sym, int, uint32_t mant) {
-    atomicAdd(&hac[sym], 1u);
+    atomicAdd(&hac[sym & 127], 1u << ((sym >> 7) << 4));
     rec[n * 64] = ((uint32_t)sym << 16) | mant;
     n++;
   }
@@ -529,6 +536,20 @@ struct CountSink {
   __device__ __forceinline__ void put_ac(uint32_t, int sym, int cat, uint32_t mant) { ac(sym, cat, mant); }
   __device__ __forceinline__ void finish() {}
 };
+
+// The wave's 16-bit counter pairs (CountSink) added into the frame's table block hf, and zeroed.
+__device__ __forceinline__ void flush_counts(uint32_t *s_cnt, uint32_t *hf, int lane) {
+  for (int i = lane; i < kCountWords; i += 64) {
+    const uint32_t v = s_cnt[i];
+    if (v) {
+      const int lo = i < 256 ? (i >> 7) * 256 + (i & 127) : 512 + ((i - 256) >> 3) * 16 + (i & 7);
+      const int hi = lo + (i < 256 ? 128 : 8);
+      if (v & 0xffffu) atomicAdd(&hf[lo], v & 0xffffu);
+      if (v >> 16) atomicAdd(&hf[hi], v >> 16);
+      s_cnt[i] = 0;
+    }
+  }
+}
 
 // Raw 8x8 block as 8 little-endian row words.  Addresses are 32-bit offsets from the frame's
 // base, which is wave-uniform (a chunk never spans two frames): the loads take the base from
@@ -1182,14 +1203,15 @@ struct XcdUnits {
 // DBG: the MJG_F_DEBUG_COEFS instantiation (quantised blocks out); the product kernels carry
 // neither its branch nor its live scalars (k_encode is short of SGPRs: they spill to VGPR lanes).
 template <bool RC, int MODE, bool MF = false, bool DBG = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
-__global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
+__global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPerEU) void k_encode(
     const SegList frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
     int16_t *__restrict__ dbg_coefs, uint32_t *__restrict__ work_ctr, int ntasks,
     uint32_t *__restrict__ hist, uint32_t *__restrict__ stage_all,
     uint32_t *__restrict__ syms, uint32_t *__restrict__ symn) {
-  __shared__ uint32_t s_ac[512];
-  __shared__ uint32_t s_dc[32];
+  constexpr bool EM = MODE == kEmitDefault;  // the AC / DC codes (the counting pass codes nothing)
+  __shared__ uint32_t s_ac[EM ? 512 : 1];
+  __shared__ uint32_t s_dc[EM ? 32 : 1];
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ uint4 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
@@ -1204,12 +1226,14 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   // emit_block_wave's stream words, pack_chunk_short's chunk words
   __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kHvWords];
-  // per wave: the current frame's histogram (kCount)
-  __shared__ uint32_t s_aux_all[MODE == kEmitDefault ? 1 : kWavesPerWg][MODE == kEmitDefault ? 1 : kFrameTabWords];
+  // per wave: the current frame's histogram (kCount; CountSink's 16-bit pairs)
+  __shared__ uint32_t s_aux_all[EM ? 1 : kWavesPerWg][EM ? 1 : kCountWords];
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
-  if (tid < 32) s_dc[tid] = tabs[512 + tid];
+  if (EM) {
+    for (int i = tid; i < 512; i += 64 * kWavesPerWg) s_ac[i] = tabs[i];
+    if (tid < 32) s_dc[tid] = tabs[512 + tid];
+  }
   if (tid < 64) {
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
@@ -1234,8 +1258,9 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     for (int i = lane; i < kHvWords; i += 64) s_hv[i] = 0u;
   uint32_t *s_aux = s_aux_all[MODE == kEmitDefault ? 0 : wave];
   if (MODE == kCount)
-    for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = 0;
+    for (int i = lane; i < kCountWords; i += 64) s_aux[i] = 0;
   int aux_frame = -1;  // frame whose histogram / tables s_aux holds (wave-uniform)
+  int aux_chunks = 0;  // chunks counted into s_aux since its last flush
   __syncthreads();  // tables visible; the only workgroup barrier
 
   const int gw = blockIdx.x * kWavesPerWg + wave;
@@ -1325,20 +1350,17 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
     const int diff = dc - dc_predictor(dc, carry, desc_delta(dsc), cur_chunk == 0, lane);
     carry = dc;
 
-    if (MODE == kCount && cur_frame != aux_frame) {  // flush the previous frame's counts
+    if (MODE == kCount && (cur_frame != aux_frame || aux_chunks == kCountFlush)) {  // flush the counts
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS traffic is done
-      if (aux_frame >= 0)
-        for (int i = lane; i < kFrameTabWords; i += 64) {
-          const uint32_t v = s_aux[i];
-          if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
-          s_aux[i] = 0;
-        }
+      if (aux_frame >= 0) flush_counts(s_aux, hist + (size_t)aux_frame * kFrameTabWords, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       aux_frame = cur_frame;
+      aux_chunks = 0;
     }
     if (MODE == kCount) {
-      CountSink cs{s_aux + tab * 256, s_aux + 512 + tab * 16, syms + (size_t)t * kSymCap * 64 + lane};
+      CountSink cs{s_aux + tab * 128, s_aux + 256 + tab * 8, syms + (size_t)t * kSymCap * 64 + lane};
       if (cur_active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
+      aux_chunks++;
       symn[(size_t)t * 64 + lane] = cs.n;
       if (tn < 0) break;
       if (new_batch) {
@@ -1387,10 +1409,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, kEncWavesPerEU) void k_encode(
   }
   if (MODE == kCount && aux_frame >= 0) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int i = lane; i < kFrameTabWords; i += 64) {
-      const uint32_t v = s_aux[i];
-      if (v) atomicAdd(&hist[(size_t)aux_frame * kFrameTabWords + i], v);
-    }
+    flush_counts(s_aux, hist + (size_t)aux_frame * kFrameTabWords, lane);
   }
 }
 
