@@ -177,12 +177,13 @@ constexpr int kSlots = 2;
 // so the launch's ramp and drain (T(n) = 0.115 ms + 4.48 us n per 4K launch) is
 // paid once per kMerge submits.  Each submit stays a job of its own for mjg_sync / mjg_fetch.
 constexpr int kMerge = 2;
-// k_emit_syms workgroups per k_encode workgroup: the replay waits on its record loads most of
-// its time (SQ_WAIT_ANY 72% of its wave cycles, profiles/r05/head_sq_c1.json) and needs 54
-// VGPRs and 8.7 KB of LDS, so more waves per SIMD than k_encode's four hide that latency.
-// bench c1 (profiles/r05/c1_emit_grid_bench.txt): x1 390-396K fps, x2 410-415K, x4 418-421K,
-// x8 405-418K; k_emit_syms alone 0.258 / 0.261 / 0.210 / 0.190 ms per 250 1080p frames
-constexpr int kEmitGridMul = 4;
+// k_emit_syms workgroups per k_encode workgroup: the replay waits on memory most of its time
+// and needs 54 VGPRs and 8.7 KB of LDS, so more waves per SIMD than k_encode's four hide that
+// latency.  Since each wave replays a run of consecutive chunks (one table load per frame
+// instead of one per chunk), x2 is the best grid: bench c1 x1 / x2 / x4 0.526-0.529 /
+// 0.508-0.512 / 0.506-0.522 ms per step (profiles/r05/c1_emit_runs_ab.txt; with strided chunks
+// x4 was best, profiles/r05/c1_emit_grid_bench.txt)
+constexpr int kEmitGridMul = 2;
 // merging is off when the slots' doubled scratch would take more than this share of the
 // device's free memory (slot buffers scale with the frames a launch may carry)
 constexpr double kMergeMemShare = 0.25;
@@ -770,10 +771,8 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       &per_cu, c->dct_mfma ? (const void *)k_encode<true, kEmitDefault, true> : (const void *)k_encode<true, kEmitDefault>,
       64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
-  // -huffman optimal's counting pass (per-wave histograms: 3 workgroups fit per CU) is launched
-  // with the same grid: the fourth workgroup of a CU starts as the first to finish leaves and
-  // pulls the units left; sized to its own occupancy it measured 1.8% slower on c1
-  // (profiles/r04an_c1_count_grid_tail_prio.txt)
+  // -huffman optimal's counting pass is launched with the same grid (4 workgroups per CU: its
+  // histograms are 16-bit counter pairs, profiles/r05/c1_count_occupancy_ab.txt)
   c->enc_grid_cnt = c->enc_grid;
   c->stage_cols = (size_t)c->enc_grid * kWavesPerWg * (c->optimal ? kEmitGridMul : 1);
   return alloc_slot(c, c->slot[0]);

@@ -1442,13 +1442,16 @@ __global__ __launch_bounds__(64 * kWavesPerWg) void k_emit_syms(
 #pragma unroll
     for (int i = 0; i < 8; i++) e_nx[i] = rec[i * 64];
   };
-  if (gw < ntasks) head(gw);
-  for (int t = gw; t < ntasks; t += nwaves) {
+  // a wave takes a run of consecutive chunks: one frame's tables serve the whole run (taking
+  // every nwaves-th chunk reloaded the tables for every chunk)
+  const int per = (ntasks + nwaves - 1) / nwaves, t0 = gw * per, t1 = min(t0 + per, ntasks);
+  if (t0 < t1) head(t0);
+  for (int t = t0; t < t1; t++) {
     int frame, chunk, bbase;
     task_pos(g, t, frame, chunk, bbase);
     const uint32_t n = n_nx;
     uint32_t e[8] = {e_nx[0], e_nx[1], e_nx[2], e_nx[3], e_nx[4], e_nx[5], e_nx[6], e_nx[7]};
-    if (t + nwaves < ntasks) head(t + nwaves);
+    if (t + 1 < t1) head(t + 1);
     if (frame != aux_frame) {  // the frame's code tables into the wave's LDS
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (int i = lane; i < kFrameTabWords; i += 64) s_aux[i] = ftabs[(size_t)frame * kFrameTabWords + i];
