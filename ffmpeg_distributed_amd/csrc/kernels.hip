@@ -551,6 +551,58 @@ __device__ __forceinline__ void flush_counts(uint32_t *s_cnt, uint32_t *hf, int 
   }
 }
 
+// Wave-parallel counting of one block h (wave-uniform), CountSink's work for the blocks
+// wave_parallel_blocks picks: lane k quantises zigzag coefficient k as emit_block_wave does and
+// holds its ZRLs + (run, size) symbol (lane 0 the DC, lane 63 the EOB); a prefix sum of the
+// lanes' symbol counts places each lane's records in block h's record column (the records and
+// order of emit_block with CountSink), and each lane counts its symbols.  Returns the block's
+// symbol count.
+__device__ __noinline__ uint32_t count_block_wave(const uint32_t *s_pk, int h, int diff_h, int tab_h,
+                                                  const uint4 *zd, const uint32_t *m2, uint32_t *s_cnt,
+                                                  uint32_t *rec_h, int lane) {
+  const uint32_t wv = lane < 32 ? s_pk[lane * 64 + h] : 0u;
+  const uint4 d = zd[lane];
+  const uint32_t cw = d.w >> 6;
+  const uint4 mp = *(const uint4 *)((const uint8_t *)m2 + d.z);
+  const uint32_t m[4] = {mp.x, mp.y, mp.z, mp.w};
+  int acc = (int)d.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t pr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)cw + 4 * i, (int)wv);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr), __builtin_bit_cast(short2_t, m[i]), acc, false);
+  }
+  const int u = acc >> 17;
+  int t = (__mul24(u, (int)d.y) + (u < 0 ? -1 - (3 << 18) : (3 << 18))) >> 21;  // exact_coef_t
+  if (lane == 0) t = 0;
+  const int fb = ffbh_i32(t);
+  const uint64_t nz = __ballot(fb >= 0);
+  uint32_t *hac = s_cnt + tab_h * 128;
+  uint32_t nsym = 0, zrl = 0, r = 0;  // this lane's symbols, its ZRLs among them, its last record
+  if (fb >= 0) {
+    const uint64_t below = nz & ((1ull << lane) - 1ull);
+    const int run = lane - (below ? 63 - (int)__builtin_clzll(below) : 0) - 1;
+    zrl = (uint32_t)run >> 4;
+    const int cat = 32 - fb, sym = ((run & 15) << 4) | cat;
+    r = ((uint32_t)sym << 16) | __builtin_amdgcn_ubfe((uint32_t)t, 0u, (uint32_t)cat);
+    nsym = zrl + 1;
+    atomicAdd(&hac[sym & 127], 1u << ((sym >> 7) << 4));
+    if (zrl) atomicAdd(&hac[0xf0 & 127], zrl << 16);  // ZRL 0xf0: word 0x70, high half
+  } else if (lane == 63) {  // EOB: coefficient 63 is zero
+    nsym = 1;
+    atomicAdd(&hac[0], 1u);
+  } else if (lane == 0) {
+    uint32_t mant = 0;
+    const int cat = diff_h ? mag_cat(diff_h, mant) : 0;
+    r = (1u << 31) | ((uint32_t)cat << 16) | mant;
+    nsym = 1;
+    atomicAdd(&s_cnt[256 + tab_h * 8 + (cat & 7)], 1u << ((cat >> 3) << 4));
+  }
+  const uint32_t incl = wave_incl_scan(nsym, lane), off = incl - nsym;
+  for (uint32_t i = 0; i < zrl; i++) rec_h[(off + i) * 64] = 0xf0u << 16;
+  if (nsym) rec_h[(off + nsym - 1) * 64] = r;
+  return lane63(incl);
+}
+
 // Raw 8x8 block as 8 little-endian row words.  Addresses are 32-bit offsets from the frame's
 // base, which is wave-uniform (a chunk never spans two frames): the loads take the base from
 // SGPRs and one VGPR offset (global_load saddr form), no 64-bit address arithmetic per row.
@@ -1359,9 +1411,19 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
     }
     if (MODE == kCount) {
       CountSink cs{s_aux + tab * 128, s_aux + 256 + tab * 8, syms + (size_t)t * kSymCap * 64 + lane};
-      if (cur_active) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
+      // the heavy blocks wave-parallel, as the default-table encode codes them
+      const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);
+      if (cur_active && !((wide >> lane) & 1ull)) emit_block(s_pk + lane, mask, diff, s_zd, s_m2, cs);
+      uint32_t nsym = cs.n;
+      for (uint64_t hw = wide; hw; hw &= hw - 1) {
+        const int h = (int)__builtin_ctzll(hw);
+        const uint32_t nh = count_block_wave(s_pk, h, __builtin_amdgcn_readlane(diff, h),
+                                             __builtin_amdgcn_readlane(tab, h), s_zd, s_m2, s_aux,
+                                             syms + (size_t)t * kSymCap * 64 + h, lane);
+        if (lane == h) nsym = nh;
+      }
       aux_chunks++;
-      symn[(size_t)t * 64 + lane] = cs.n;
+      symn[(size_t)t * 64 + lane] = nsym;
       if (tn < 0) break;
       if (new_batch) {
         carry = carry_finish(crow, chunk, lane, rc, g, s_desc);

@@ -769,9 +769,11 @@ def _sweep(cases, **opts):
             assert got[i] == ref[i], (c, i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
+@pytest.mark.parametrize("huffman", ["default", "optimal"])
 @pytest.mark.parametrize("q,full", [(1, False), (3, True), (8, False), (20, True)])
-def test_wave_parallel_blocks_match_oracle(q, full):
-    """k_encode's wave-parallel emission (emit_block_wave, default tables): chunks with 1..14
+def test_wave_parallel_blocks_match_oracle(q, full, huffman):
+    """k_encode's wave-parallel emission (emit_block_wave, default tables) and the counting
+    pass's wave-parallel counting (count_block_wave, -huffman optimal): chunks with 1..14
     heavy blocks among flat ones -- noise of amplitudes 2..128 (dense blocks with coefficient
     63 set, and sparse ones with long zero runs, i.e. ZRLs), luma and chroma -- byte-equal to
     the oracle."""
@@ -801,9 +803,9 @@ def test_wave_parallel_blocks_match_oracle(q, full):
         frames.append(pack_i420(y.clip(0, 255).astype(np.uint8), u.clip(0, 255).astype(np.uint8),
                                 v.clip(0, 255).astype(np.uint8)))
     frames = np.stack(frames)
-    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=n) as enc:
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=n, huffman=huffman) as enc:
         got = enc.encode(frames)
-    ref = oracle_frames(frames, w, h, q, full)
+    ref = oracle_frames(frames, w, h, q, full, huffman=huffman)
     for i in range(n):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
