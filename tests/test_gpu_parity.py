@@ -5,6 +5,8 @@ against FFmpeg itself is unpinned (FFmpeg is absent on this pool).
 """
 import io
 
+import os
+
 import numpy as np
 import pytest
 
@@ -753,6 +755,12 @@ def test_random_sweep_matches_oracle(part):
 def test_random_sweep_large_matches_oracle(part):
     """48 more seeded random configurations at 8..2200 x 8..1300 (one frame each)."""
     _sweep(SWEEP_LARGE[part::4])
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_random_sweep_more_seeds(seed):
+    """600 more seeded random configurations per seed, as the sweep above (~3 s each)."""
+    _sweep(_sweep_cases(seed=seed))
 
 
 def _sweep(cases, **opts):
