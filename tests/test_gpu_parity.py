@@ -893,6 +893,23 @@ def test_dct_mfma_4k_segment_from_device_memory():
         assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
 
 
+# ------------------------------------------- a long -huffman optimal launch
+def test_optimal_long_launch_matches_oracle():
+    """120 1080p frames in one -huffman optimal launch (8 distinct testsrc2 frames, plus noise
+    frames, cycled): ~92K chunks, so the counting pass's waves take several units each and flush
+    their 16-bit counters every 16 chunks within a frame as well as at frame changes; every frame
+    byte-equal to the oracle's encoding of its source."""
+    w, h, n = 1920, 1080, 120
+    src = [make_testsrc(w, h, t) for t in range(6)] + list(rand_frames(w, h, 2, seed=77, kind="noise"))
+    frames = np.stack([src[i % len(src)] for i in range(n)])
+    ref = oracle_frames(np.stack(src), w, h, 5, False, huffman="optimal")
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=n, huffman="optimal") as enc:
+        got = enc.encode(frames)
+    for i in range(n):
+        r = ref[i % len(src)]
+        assert got[i] == r, (i, len(got[i]), len(r), first_diff(got[i], r))
+
+
 # ------------------------------------------- k_huff_build on given counts (mjg_debug_huff_build)
 def test_huff_build_matches_oracle_tables():
     """-huffman optimal's table builder alone, on the 153 count vectors the CPU tests pin the
