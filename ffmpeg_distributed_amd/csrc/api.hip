@@ -152,6 +152,7 @@ int dmalloc(T **p, size_t count) {
 struct PlaneScale {
   SwsFilter hf, vf;
   int32_t *hcp = nullptr, *hp = nullptr, *vcp = nullptr, *vps = nullptr, *hsum = nullptr;
+  int32_t *mfb = nullptr;  // k_scale's matrix-core h-pass: the B fragments (ScaleGeom::mf_*)
   bool d4 = false;  // h coefficients in the v_dot4 hi/lo byte layout (k_scale D4)
   ScaleGeom g{};
   size_t lds = 0;
@@ -278,7 +279,7 @@ void free_ctx(mjg_ctx *c) {
   if (c->tail) (void)hipStreamSynchronize(c->tail);
   void *ptrs[] = {c->d_tabs, c->d_hdr, c->ps[0].hcp,
                   c->ps[0].vcp, c->ps[0].hp, c->ps[0].vps, c->ps[1].hcp, c->ps[1].vcp, c->ps[1].hp,
-                  c->ps[0].hsum, c->ps[1].hsum, c->ps[1].vps};
+                  c->ps[0].hsum, c->ps[1].hsum, c->ps[1].vps, c->ps[0].mfb, c->ps[1].mfb};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (Slot &S : c->slot) {
@@ -388,7 +389,8 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   g.lds_pairs = max_pairs;
   if (th >= 64) {  // pair image over the window rows (scale.hip: ALIAS)
     g.lds_win_words = 2 * max_pairs * kScaleAliasWords;
-    p.lds = (size_t)g.lds_win_words * 4;  // v filter rows by scalar loads
+    p.lds = (size_t)g.lds_win_words * 4 + 64;  // v filter rows by scalar loads; the matrix-core
+                                               // h-pass reads 16 bytes past the last row
   } else {
     g.lds_win_words = 2 * max_pairs * max_nw;
     p.lds = ((size_t)g.lds_win_words + (size_t)max_pairs * kScaleTileW + (size_t)th * (npv + 1)) * 4;
@@ -406,6 +408,40 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
   HIP_TRY(hipMemcpy(p.hp, p.hf.pos.data(), (size_t)dw * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(p.vcp, vcp.data(), vcp.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(p.vps, vps.data(), (size_t)dh * 4, hipMemcpyHostToDevice));
+  // The matrix-core h-pass (scale.hip, scale_hpass_mf) for the interior tile columns when they
+  // all share one filter at a 2-byte step (exact 2:1): B[k][n] = the hi (lo) byte of tap
+  // k - 2n - d of that filter (0 outside the 8 taps), k the byte of a 64-byte window that starts
+  // at the column block's aligned byte 32 cj, d = the first column's byte offset in its dword.
+  // Lane l holds B[16 (l >> 4) + j][l & 15] in byte j (the same k map as its A fragment).
+  g.mf_bx0 = g.mf_bx1 = 0;
+  g.mf_hs = 0;
+  const int gxt = (dw + kScaleTileW - 1) / kScaleTileW;
+  if (p.d4 && ht == 8 && th >= 64 && gxt >= 3) {
+    const int xa = kScaleTileW, xb = kScaleTileW * (gxt - 1);
+    bool ok = true;
+    for (int x = xa; x < xb && ok; x++) {
+      ok = p.hf.pos[x] == p.hf.pos[xa] + 2 * (x - xa) && hsum[x] == hsum[xa];
+      for (int k = 0; k < ht / 2 && ok; k++) ok = hcp[(size_t)x * (ht / 2) + k] == hcp[(size_t)xa * (ht / 2) + k];
+    }
+    if (ok) {
+      const int d = p.hf.pos[xa] & 3;
+      std::vector<int32_t> mfb(64 * 8, 0);
+      for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 16; j++) {
+          const int k = 16 * (l >> 4) + j, n = l & 15, t = k - 2 * n - d;
+          if (t < 0 || t >= 8) continue;
+          const uint32_t hi = ((uint32_t)hcp[(size_t)xa * (ht / 2) + 2 * (t >> 2)] >> (8 * (t & 3))) & 255u;
+          const uint32_t lo = ((uint32_t)hcp[(size_t)xa * (ht / 2) + 2 * (t >> 2) + 1] >> (8 * (t & 3))) & 255u;
+          mfb[(size_t)l * 8 + (j >> 2)] |= (int32_t)(hi << (8 * (j & 3)));
+          mfb[(size_t)l * 8 + 4 + (j >> 2)] |= (int32_t)(lo << (8 * (j & 3)));
+        }
+      if ((rc = dmalloc(&p.mfb, mfb.size()))) return rc;
+      HIP_TRY(hipMemcpy(p.mfb, mfb.data(), mfb.size() * 4, hipMemcpyHostToDevice));
+      g.mf_bx0 = 1;
+      g.mf_bx1 = gxt - 1;
+      g.mf_hs = hsum[xa];
+    }
+  }
   (void)c;
   return MJG_OK;
 }
@@ -960,13 +996,13 @@ int submit_impl(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device, con
   do {                                                                                              \
     if (sg.range == 1)                                                                              \
       k_scale<HT, NPV, D4, 1, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(in_sl, S.d_scaled, sg, ps.hcp,        \
-                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum); \
+                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum, ps.mfb); \
     else if (sg.range == 2)                                                                         \
       k_scale<HT, NPV, D4, 2, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(in_sl, S.d_scaled, sg, ps.hcp,        \
-                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum); \
+                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum, ps.mfb); \
     else                                                                                            \
       k_scale<HT, NPV, D4, 0, TH><<<grid, 64 * scale_waves(TH), ps.lds, S.st>>>(in_sl, S.d_scaled, sg, ps.hcp,        \
-                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum); \
+                                                                    ps.hp, ps.vcp, ps.vps, ps.hsum, ps.mfb); \
   } while (0)
 #define MJG_SCALE_LAUNCH(HT, NPV, TH)      \
   do {                                     \

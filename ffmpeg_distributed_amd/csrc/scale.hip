@@ -35,6 +35,7 @@
 namespace mjg {
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kScaleTileW = 64;
 constexpr int kScaleLoadRows = 7;  // fast window path: rows x 9 pieces per wave-instruction
@@ -62,6 +63,8 @@ struct ScaleGeom {
   // multiply-high with ceil(2^32 / d), not by two scalar divisions (div_magic)
   int gx, gxy;
   uint32_t gx_magic, gxy_magic;  // 0 when the divisor is 1
+  int mf_bx0, mf_bx1, mf_hs;     // tile columns [mf_bx0, mf_bx1) take the matrix-core h-pass
+                                 // (one filter, hsum mf_hs; the host checks: api.hip)
 };
 
 // t / d for 0 <= t < 2^31: with m = ceil(2^32 / d), umulhi(t, m) is t / d or one more (the
@@ -128,7 +131,8 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const SegList sr
                                                const int32_t *__restrict__ hp,    // [dw]
                                                const int32_t *__restrict__ vcp,   // [dh][npv]
                                                const int32_t *__restrict__ vps,   // [dh] pair start
-                                               const int32_t *__restrict__ hsum) {  // D4: [dw] sum of taps
+                                               const int32_t *__restrict__ hsum,  // D4: [dw] sum of taps
+                                               const int32_t *__restrict__ mfb) {  // matrix-core h-pass B fragments
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   constexpr int LPW = scale_loads_per_wave(TH), NWV = scale_waves(TH), NT = 64 * NWV;
   constexpr bool ALIAS = TH >= 64;
@@ -170,12 +174,72 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const SegList sr
   const int np = p1 - p0, ppw = ALIAS ? (np + NWV - 1) / NWV : 0;
   const bool fast = nw <= 36 && g.sw >= 16 &&
                     (ALIAS ? 2 * ppw <= LPW * kScaleLoadRows : nrows <= NWV * LPW * kScaleLoadRows);
+  const int rr = lane / 9, pc = lane - 9 * rr, col = cb + 16 * pc;  // fast loads: row, piece
+  // The matrix-core h-pass (2:1 interior tiles): the window is loaded as on the VALU path, then
+  // wave w computes column block w (16 output columns) of every 16-row block of the window as
+  // v_mfma_i32_16x16x64_i8 products: A = 16 window rows x 64 bytes from the column block's
+  // aligned byte 32 w (one ds_read_b128 per lane: lane l row l & 15, bytes 16 (l >> 4) .. +15),
+  // B = the shared filter's hi / lo tap bytes on the band (host-built, the same k map), so D =
+  // ah / al of hscale_lds for rows 4 (l >> 4) + i, column l & 15.  Every wave reads every row,
+  // so the pairs are written over the window after a barrier.
+  if (TH == 64 && D4 && HT == 8 && fast && bx >= g.mf_bx0 && bx < g.mf_bx1) {
+    const int ppw2 = (p1 - p0 + NWV - 1) / NWV;  // the VALU path's row split for the loads
+    u32x4 wv[LPW];
+#pragma unroll
+    for (int i = 0; i < LPW; i++) {
+      const int r = 2 * ppw2 * wave + kScaleLoadRows * i + rr;
+      const uint8_t *rp = s + (size_t)min(2 * p0 + r, g.sh - 1) * g.s_stride;
+      if (col + 16 <= g.sw) {
+        wv[i] = *(const u32x4_a1 *)(rp + col);
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int cc = col + 4 * k, lc = min(cc, g.sw - 4);
+          w[k] = cc < g.sw ? *(const u32_unaligned *)(rp + lc) >> ((cc - lc) * 8) : 0u;
+        }
+        wv[i] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    }
+    const u32x4 bhi = ((const u32x4 *)mfb)[2 * lane], blo = ((const u32x4 *)mfb)[2 * lane + 1];
+#pragma unroll
+    for (int i = 0; i < LPW; i++) {
+      const int r = 2 * ppw2 * wave + kScaleLoadRows * i + rr;
+      if (rr < kScaleLoadRows && r < nrows && 4 * pc < nw && kScaleLoadRows * i + rr < 2 * ppw2)
+        *(u32x4 *)(win + r * rs + 4 * pc) = wv[i] ^ 0x80808080u;
+    }
+    __syncthreads();
+    const int g4 = lane >> 4, n = lane & 15;
+    constexpr int kMfBlocks = 9;  // 16-row blocks: >= the 136 rows of a 64-row tile
+    uint32_t pk[kMfBlocks][2];
+#pragma unroll
+    for (int m = 0; m < kMfBlocks; m++) {
+      pk[m][0] = pk[m][1] = 0u;
+      if (16 * m < nrows) {
+        const int row = min(16 * m + n, nrows - 1);
+        const v4i av = __builtin_bit_cast(v4i, *(const u32x4 *)(win + row * rs + 8 * wave + 4 * g4)), z = {0, 0, 0, 0};
+        const v4i hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, __builtin_bit_cast(v4i, bhi), z, 0, 0, 0);
+        const v4i lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, __builtin_bit_cast(v4i, blo), z, 0, 0, 0);
+        int h[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) h[i] = sws_range(min(hi[i] + (lo[i] >> 7) + g.mf_hs, 32767), RANGE);
+        pk[m][0] = ((uint32_t)h[0] & 0xffffu) | ((uint32_t)h[1] << 16);
+        pk[m][1] = ((uint32_t)h[2] & 0xffffu) | ((uint32_t)h[3] << 16);
+      }
+    }
+    __syncthreads();  // every wave's window reads done: the pairs go over the rows
+#pragma unroll
+    for (int m = 0; m < kMfBlocks; m++) {
+      const int pa = 8 * m + 2 * g4;  // the pairs of D rows 4 g4 .. 4 g4 + 3 of block m
+      if (pa < np) pairs[pa * ps + 16 * wave + n] = pk[m][0];
+      if (pa + 1 < np) pairs[(pa + 1) * ps + 16 * wave + n] = pk[m][1];
+    }
+  } else {
   // Every global load of the tile is issued before any is waited on: the window rows, this
   // lane's h filter (column x), and the tile's v filter rows (one entry per thread).
   // fast path: 16-byte pieces, 7 rows of 9 pieces per wave-instruction, 3 per wave (84 rows
   // of <= 144 bytes)
   u32x4 v[LPW];
-  const int rr = lane / 9, pc = lane - 9 * rr, col = cb + 16 * pc;
   if (fast) {
 #pragma unroll
     for (int i = 0; i < LPW; i++) {
@@ -254,6 +318,7 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const SegList sr
     }
     pairs[p * ps + lane] = ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16);
   }
+  }  // (the VALU h-pass)
   __syncthreads();
   if (x0 + lane >= g.dw) return;
   for (int y = y0 + wave; y < ye; y += NWV) {
