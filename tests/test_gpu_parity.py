@@ -132,6 +132,20 @@ def test_encode_huffman_optimal_matches_oracle(w, h, q, full, kind):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
+@pytest.mark.parametrize("kind,full", [("noise", False), ("checker", True), ("testsrc", False), ("smooth", True)])
+def test_scale_2to1_matrix_core_hpass(kind, full):
+    """Exact 2:1 downscales take k_scale's matrix-core h-pass on their interior tile columns
+    (every column but the first and last 64): extreme pixels (noise, checker: the largest h sums
+    and the range clamps) and smooth content, tv and pc range, byte-equal to the oracle."""
+    w, h, n = 1536, 768, 2
+    frames = rand_frames(w, h, n, seed=91, kind=kind)
+    with MjpegEncoder(0, w, h, w // 2, h // 2, qscale=4, full_range=full, max_batch=n) as enc:
+        got = enc.encode(frames)
+    ref = oracle_frames(frames, w, h, 4, full, w // 2, h // 2)
+    for i in range(n):
+        assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
+
+
 def test_huffman_optimal_scaled_batches():
     """optimal tables with -vf scale, ragged batches and a reused context."""
     sw, sh, dw, dh, q = 160, 96, 80, 48, 3
