@@ -33,7 +33,11 @@ def _command(out: str):
     # compiler emits the three-operand v_dot4_i32_i8 / v_dot2_i32_i16, which take the accumulator
     # (or an SGPR) as a separate operand: no v_mov to copy a shared start value into every
     # accumulator (k_scale_encode's h-pass: 2 per output).  The host compile ignores them.
+    # -amdgpu-mfma-vgpr-form: MFMA results in VGPRs, not AGPRs (no v_accvgpr_read per result
+    # element in k_scale's matrix-core h-pass: c4 +0.8..2.2%, profiles/r05/c4_scale_mfma_vgpr_form_ab.txt;
+    # the default-table k_encode's code is unchanged).
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-mfma-vgpr-form=1",
            "-Xclang", "-target-feature", "-Xclang", "-dot6-insts",
            "-Xclang", "-target-feature", "-Xclang", "-dot4-insts",
            "-Wno-unused-command-line-argument", "-I", os.path.join(ROOT, "include"), "-o", out]
