@@ -460,6 +460,10 @@ def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
     overlap included, and bench.py adds isolated launches beside them."""
     src_b, dst_b, jpeg_b = frame_bytes(W, H) * fpl, frame_bytes(DW, DH) * fpl, mean_jpeg * fpl
     sstep = (seg or fpl) / fpl  # one step's share of a launch's bytes
+
+    def per_step(tr):
+        # the primary entry's bytes and traffic are one step's when it is timed per step
+        return None if tr is None else round(tr * sstep) if step_ms else tr
     out = []
     if scaled:  # k_scale writes the scaled planes to HBM, k_encode reads them
         out.append(roofline_entry("k_scale", src_b + dst_b, kt["scale"], pmc_traffic(pmc, fpl, "k_scale"),
@@ -476,7 +480,7 @@ def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
         primary = roofline_entry("count pass + emission (k_encode<count>, k_huff_build, k_emit_syms)"
                                  + (", wall time per step" if step_ms else ""),
                                  (enc_in + jpeg_b) * (sstep if step_ms else 1), step_ms or (kt["huff"] + kt["encode"]),
-                                 pmc_traffic(pmc, fpl, "k_encode", "k_huff_build", "k_emit_syms"),
+                                 per_step(pmc_traffic(pmc, fpl, "k_encode", "k_huff_build", "k_emit_syms")),
                                  "input planes read + JPEG written")
     else:
         name = "k_encode"
@@ -487,11 +491,11 @@ def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
         primary = out[0]
         if scaled and step_ms:
             primary = roofline_entry("k_scale + k_encode, wall time per step", (src_b + jpeg_b) * sstep, step_ms,
-                                     None, "source planes read + JPEG written")
+                                     per_step(pmc_traffic(pmc, fpl, "k_scale", "k_encode")),
+                                     "source planes read + JPEG written")
         elif step_ms:
-            tr = out[0]["traffic"]
             primary = roofline_entry(name + ", wall time per step (launches overlap)", (enc_in + jpeg_b) * sstep,
-                                     step_ms, None if tr is None else round(tr * sstep), out[0]["bytes"])
+                                     step_ms, per_step(out[0]["traffic"]), out[0]["bytes"])
     return primary, out
 
 
