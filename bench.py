@@ -79,8 +79,6 @@ def parse():
     p.add_argument("--segments-per-launch", action="store_true",
                    help="also time K = 2, 4 segments per submit (mjg_submit_segments, N=1 only); off by "
                         "default so a profile of the default command holds only the headline's launches")
-    p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto",
-                   help="-huffman default: k_encode's DCT stage (auto: the VALU passes; mfma: the matrix cores)")
     p.add_argument("--no-kernel-timing", action="store_true", help="diagnostics: no HIP events at all")
     p.add_argument("--kernel-timing-detail", action="store_true",
                    help="events around every tail kernel too (adds ~10 us idle per event)")
@@ -557,8 +555,7 @@ def main():
 
     enc = MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=seg,
                        timing=False if a.no_kernel_timing else ("detail" if a.kernel_timing_detail else True),
-                       huffman=HUFF, rst=a.rst,
-                       dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
+                       huffman=HUFF, rst=a.rst, merge=True)
     bytes_out = []
 
     # Segments are pipelined enc.depth (mjg_queue_depth(): 2) deep, as mjg_submit queues them: later segments'
@@ -619,8 +616,7 @@ def main():
     mean_jpeg = sum(bytes_out) / max(1, len(bytes_out) * seg)
     fpl = a.steps * seg / nl if nl else seg  # frames per launch (merged launches carry two segments)
     pmc, pmc_src = (load_pmc(a.workload, a.content, B.source_digest())
-                    if (seg == SEG and not a.rst and a.dct == "auto"
-                        and HUFF == WORKLOADS[a.workload][7]) else ({}, "no PMC pass for this configuration"))
+                    if (seg == SEG and not a.rst and HUFF == WORKLOADS[a.workload][7]) else ({}, "no PMC pass for this configuration"))
     overlap = True  # consecutive launches run on two streams (csrc/api.hip alloc_slot; see rooflines)
     primary, per_kernel = rooflines(kt, fpl, mean_jpeg, pmc, HUFF == "optimal", (DW, DH) != (W, H),
                                     dt / a.steps * 1e3 if overlap else None, seg)
@@ -636,8 +632,7 @@ def main():
             if k > nseg_pool:
                 continue
             e2 = enc if k == 1 else MjpegEncoder(local, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=k * seg,
-                                                  timing=True, huffman=HUFF, rst=a.rst, merge=False,
-                                                  dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
+                                                  timing=True, huffman=HUFF, rst=a.rst, merge=False)
             e2.kernel_times(reset=True)
             for r in range(4):
                 segs = [(pool[((r * k + i) % nseg_pool) * seg].data_ptr(), seg) for i in range(k)]
@@ -703,8 +698,7 @@ def main():
                        **({"scale_kernels": "k_scale + k_encode"}
                           if (DW, DH) != (W, H) else {}),
                        "dct": "VALU (k_encode<.., optimal counting pass>)" if HUFF == "optimal" else
-                              ("matrix cores (dct_mfma)" if a.dct == "mfma"
-                               else "VALU (row_pass + column_screen)")},
+                              "VALU (row_pass + column_screen)"},
             "roofline": primary,
             "roofline_kernels": per_kernel,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kt.items()},

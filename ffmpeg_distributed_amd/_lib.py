@@ -27,10 +27,7 @@ MJG_F_COM_ITU601 = 8
 MJG_F_HUFFMAN_OPTIMAL = 16
 MJG_F_RST = 32
 MJG_F_TIMING_DETAIL = 64
-MJG_F_FUSED = 128  # retired (r05): accepted and ignored by the library
-MJG_F_DCT_MFMA = 256
-MJG_F_DCT_VALU = 512
-MJG_F_NO_MERGE = 1024
+MJG_F_MERGE = 1024
 
 # mjg_config.chroma_format
 CHROMA_FORMATS = {"420": 0, "422": 1, "444": 2}

@@ -243,7 +243,6 @@ struct mjg_ctx {
   bool optimal = false;        // -huffman optimal
   size_t dht_pos = 0, dht_end = 0;
   PlaneScale ps[2];  // 0 luma, 1 chroma (U and V share)
-  bool dct_mfma = false;  // k_encode's DCT stage on the matrix cores (dct_mfma)
   size_t slot_B = 0, slot_NC = 0, slot_NS = 0;  // slot sizes: frames, chunks and segments per frame
 
   Slot slot[kSlots];
@@ -494,96 +493,6 @@ int alloc_slot(mjg_ctx *c, Slot &S) {
   return MJG_OK;
 }
 
-// IEEE binary16 bits of x (normal range or 0), round to nearest even; `up`: the next value
-// away from zero when that rounding shrank |x|.
-uint16_t f16_bits(double x, bool up) {
-  if (x == 0.0) return 0;
-  const uint16_t sign = x < 0 ? 0x8000 : 0;
-  double a = std::fabs(x);
-  int e = (int)std::floor(std::log2(a));
-  if (std::ldexp(1.0, e) > a) e--;
-  if (std::ldexp(1.0, e + 1) <= a) e++;
-  double m = a / std::ldexp(1.0, e - 10);  // [1024, 2048)
-  double r = std::nearbyint(m);            // ties to even (default rounding mode)
-  if (up && r < m) r += 1.0;
-  if (r >= 2048.0) {
-    r /= 2.0;
-    e++;
-  }
-  return (uint16_t)(sign | (uint16_t)((e + 15) << 10) | (uint16_t)((int)r - 1024));
-}
-
-// MF k_encode's MFMA A fragments (kernels.hip dct_mfma), [frag][lane] x 4 words of f16 pairs.
-// A1 (pass 1, exact): the pass-1 matrix in two f16 digits; A2 (pass 2, screen): the pass-2
-// rows of zigzag coefficient z scaled by 2^10 / tau_z, where tau_z is the pass-2 sum below
-// which the coefficient quantises to zero minus a bound on the screen's error:
-//   * pass-1 outputs enter as f16(D), D = S/512 + 2^-10 unrounded: |f16(D) - y| <= 0.502 +
-//     2^-11 (|y| + 1), and 0 for outputs 0/4 (multiples of 16 below 2^15: exact);
-//   * the scaled coefficients are rounded (relative 2^-11); rows 0/4 (all +-1) round up
-//     in magnitude instead, a uniform scale that only widens the screen;
-//   * f32 accumulation (2^-18 of the worst-case sum, generous);
-// with |y| <= Ymax(c) = 16384 (outputs 0/4) or 128 * L1(pass-1 row c) / 512 + 1.
-int mf_fragments(const int32_t *qmat, uint32_t *out) {
-  static const int kDot[64] = MJG_PASS2_DOT;
-  auto c1 = [&](int i, int x) { return (i == 0 || i == 4) ? 16 * kDot[i * 8 + x] : kDot[i * 8 + x]; };
-  uint16_t f[12][64][8] = {};
-  for (int l = 0; l < 64; l++) {
-    const int m = l & 31, h = l >> 5;
-    // A1: fragment 2P + d, pattern P: output row r_loc = m >> 3 takes pixel row 2P + h
-    for (int P = 0; P < 2; P++)
-      for (int d = 0; d < 2; d++)
-        for (int j = 0; j < 8; j++) {
-          const int rl = m >> 3, i = m & 7;
-          if (rl != 2 * P + h) continue;
-          const int cv = c1(i, j);
-          double v;
-          if (i == 0 || i == 4) {
-            v = d == 0 ? cv : 0;
-          } else {
-            const int hi = (int)std::lround(cv / 64.0) * 64;
-            v = (d == 0 ? hi : cv - hi) / 512.0;
-          }
-          f[2 * P + d][l][j] = f16_bits(v, false);
-        }
-    // A2: fragment 4 + 4t + s
-    for (int t = 0; t < 2; t++) {
-      const int hz = (m >> 2) & 1, q = (m & 3) + 4 * (m >> 3);
-      const int z = 32 * hz + 31 - 16 * t - q;
-      const int nat = kZigzag[z], io = nat >> 3, col = nat & 7;
-      double scale = 1.0;
-      bool up = false;
-      if (z != 0) {
-        const long long qm = qmat[nat], T = ((5ll << 18) + qm - 1) / qm;
-        const bool dcrow = io == 0 || io == 4;
-        double l1 = 0, l1c = 0;
-        for (int r = 0; r < 8; r++) l1 += std::abs(kDot[io * 8 + r]);
-        for (int x = 0; x < 8; x++) l1c += std::abs(c1(col, x));
-        const bool exact_in = col == 0 || col == 4;
-        const double ymax = exact_in ? 16384.0 : 128.0 * l1c / 512.0 + 1.0;
-        const double eb = exact_in ? 0.0 : 0.502 + (ymax + 1.0) / 2048.0;
-        const double B = dcrow ? 16.0 * (double)T - 8.5 : (double)T * 131072.0 - 65536.0 - 0.5;
-        const double E = l1 * eb + (dcrow ? 0.0 : l1 * (ymax + eb) / 2048.0) + l1 * ymax / 262144.0;
-        const double tau = B - E;
-        if (tau < 1.0) return set_err(MJG_E_INVALID, "screen threshold %g for coefficient %d", tau, z);
-        scale = 1024.0 / tau;
-        up = dcrow;
-      }
-      for (int s = 0; s < 4; s++)
-        for (int j = 0; j < 8; j++) {
-          const int nd = 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
-          const int r = 4 * (s >> 1) + (nd >> 3), i = nd & 7;
-          if (i != col) continue;
-          f[4 + 4 * t + s][l][j] = f16_bits(kDot[io * 8 + r] * scale, up);
-        }
-    }
-  }
-  for (int fr = 0; fr < 12; fr++)
-    for (int l = 0; l < 64; l++)
-      for (int e = 0; e < 4; e++)
-        out[(fr * 64 + l) * 4 + e] = (uint32_t)f[fr][l][2 * e] | ((uint32_t)f[fr][l][2 * e + 1] << 16);
-  return MJG_OK;
-}
-
 int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->device = device;
   c->cfg = *cfg;
@@ -598,6 +507,10 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
     return set_err(MJG_E_INVALID, "bad SAR %d:%d", k.sar_num, k.sar_den);
   if (k.chroma_format < MJG_CHROMA_420 || k.chroma_format > MJG_CHROMA_444)
     return set_err(MJG_E_INVALID, "chroma_format %d", k.chroma_format);
+  constexpr uint32_t kKnownFlags = MJG_F_TIMING | MJG_F_DEBUG_COEFS | MJG_F_SWS_NO_BITEXACT | MJG_F_COM_ITU601 |
+                                   MJG_F_HUFFMAN_OPTIMAL | MJG_F_RST | MJG_F_TIMING_DETAIL | MJG_F_MERGE;
+  if (k.flags & ~kKnownFlags)  // retired bits (128, 256, 512: r05's FUSED / DCT_MFMA / DCT_VALU) included
+    return set_err(MJG_E_INVALID, "unknown flags 0x%x", k.flags & ~kKnownFlags);
   if ((k.flags & MJG_F_RST) && (k.flags & MJG_F_HUFFMAN_OPTIMAL))
     return set_err(MJG_E_INVALID, "RST (slice threading) forces -huffman default");
 
@@ -665,11 +578,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   c->hdr = build_header(w, h, c->mprime, k.sar_num, k.sar_den, (k.flags & MJG_F_COM_ITU601) != 0, cf,
                         c->rst, &c->dht_pos, &c->dht_end);
   c->optimal = (k.flags & MJG_F_HUFFMAN_OPTIMAL) != 0;
-  // -huffman default: the DCT stage on the matrix cores only when MJG_F_DCT_MFMA asks for it.
-  // It was the default with -vf scale until r05; since the VALU passes' round-4 changes the VALU
-  // stage is as fast or faster there too (bench c4 155.0K vs 154.0K fps, natural +1.8%,
-  // noise-patches +13%: profiles/r05/c4_dct_stage_ab.txt)
-  c->dct_mfma = !c->optimal && !(k.flags & MJG_F_DCT_VALU) && (k.flags & MJG_F_DCT_MFMA);
 
   // device table block: [0,256) AC luma, [256,512) AC chroma, [512,528) DC luma,
   // [528,544) DC chroma ((len << 16) | code), [544,608) qmat column-major ([col][row]),
@@ -731,12 +639,6 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
       for (int i = 0; i < 3; i++) tabs[680 + 3 * (jp - 1) + i] = lim[i];
     }
   }
-  // the MFMA stage's fragments (read only by k_encode<.., MF>): when a screen threshold cannot be
-  // met the VALU stage takes over, unless MJG_F_DCT_MFMA forced the matrix cores
-  if (c->dct_mfma && mf_fragments(c->qmat, tabs + kMfTabOff) != MJG_OK) {
-    if (k.flags & MJG_F_DCT_MFMA) return MJG_E_INVALID;
-    c->dct_mfma = false;
-  }
   // [672, 680): block-of-MCU descriptors in coding order (EncGeom): plane | chroma table << 2 |
   // dx8 << 3 | dy8 << 4 | DC predecessor distance << 8 (ff_mjpeg_encode_mb order; the
   // predecessor is the previous block of the same component)
@@ -755,12 +657,14 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   }
 
   const size_t NC = (size_t)g.nchunks * g.nseg, NS = (size_t)g.nseg;
-  // merging (kMerge): off with MJG_F_NO_MERGE;
-  // MJG_MERGE=1 turns it off for a process (A/B), =2..4 sets the jobs per launch
-  c->merge = kMerge;
-  if (const char *e = getenv("MJG_MERGE")) c->merge = std::max(1, std::min(kMaxSegs, atoi(e)));
+  // merging (kMerge): opt-in with MJG_F_MERGE (a held submit's frames are read after mjg_submit
+  // returns); MJG_MERGE=1 turns it off for a process (A/B), =2..4 sets the jobs per launch
+  c->merge = 1;
+  if (k.flags & MJG_F_MERGE) {
+    c->merge = kMerge;
+    if (const char *e = getenv("MJG_MERGE")) c->merge = std::max(1, std::min(kMaxSegs, atoi(e)));
+  }
   if (const char *e = getenv("MJG_MERGE_HOLD")) c->hold_idle = atoi(e) != 0;
-  if (k.flags & MJG_F_NO_MERGE) c->merge = 1;
   if (c->merge > 1) {  // slot buffers for merge * max_batch frames: within a share of free memory
     size_t fr = 0, tot = 0;
     HIP_TRY(hipMemGetInfo(&fr, &tot));
@@ -804,8 +708,7 @@ int open_ctx(int device, const mjg_config *cfg, mjg_ctx *c) {
   int ncu = 0, per_cu = 0;
   HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, c->dct_mfma ? (const void *)k_encode<true, kEmitDefault, true> : (const void *)k_encode<true, kEmitDefault>,
-      64 * kWavesPerWg, 0));
+      &per_cu, (const void *)k_encode<true, kEmitDefault>, 64 * kWavesPerWg, 0));
   c->enc_grid = std::max(1, ncu * std::max(1, per_cu));
   // -huffman optimal's counting pass is launched with the same grid (4 workgroups per CU: its
   // histograms are 16-bit counter pairs, profiles/r05/c1_count_occupancy_ab.txt)
@@ -846,32 +749,23 @@ int launch_write(mjg_ctx *c, Slot &S, int n, bool reset_status) {
 }
 
 
-template <int MODE, bool MF, bool DBG>
-void launch_encode3(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
+template <int MODE, bool DBG>
+void launch_encode2(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
   const EncGeom &g = c->geom;
   if (g.range_convert)
-    k_encode<true, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
+    k_encode<true, MODE, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         S.d_stage_bits, S.d_syms, S.d_symn);
   else
-    k_encode<false, MODE, MF, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
+    k_encode<false, MODE, DBG><<<wgs, 64 * kWavesPerWg, 0, S.st>>>(
         enc_in, g, c->d_tabs, S.d_scratch, S.d_chunk_bits, S.d_dbg, S.d_work, ntasks, S.d_hist,
         S.d_stage_bits, S.d_syms, S.d_symn);
 }
 
-template <int MODE, bool MF>
-void launch_encode2(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
-  if (c->geom.debug_coefs)
-    launch_encode3<MODE, MF, true>(c, S, enc_in, wgs, ntasks);
-  else
-    launch_encode3<MODE, MF, false>(c, S, enc_in, wgs, ntasks);
-}
-
-// The DCT stage: the VALU passes, or (-huffman default) dct_mfma.
 template <int MODE>
 void launch_encode(mjg_ctx *c, Slot &S, const SegList &enc_in, int wgs, int ntasks) {
-  if (MODE == kEmitDefault && c->dct_mfma)
-    launch_encode2<kEmitDefault, true>(c, S, enc_in, wgs, ntasks);
+  if (c->geom.debug_coefs)
+    launch_encode2<MODE, true>(c, S, enc_in, wgs, ntasks);
   else
     launch_encode2<MODE, false>(c, S, enc_in, wgs, ntasks);
 }
@@ -1147,6 +1041,12 @@ int mjg_submit(mjg_ctx *c, const uint8_t *frames, int n, int src_is_device) {
   if (n < 1 || n > c->cfg.max_batch)
     return set_err(MJG_E_INVALID, "nframes %d not in 1..%d", n, c->cfg.max_batch);
   if (src_is_device && c->merge > 1) {  // held, and launched with the next one(s)
+    // a full held group whose launch waited at mjg_sync (its slot was the one just synced, whose
+    // results stay readable until this call): launched now, before the new job is held
+    if (c->held == c->merge && c->nout < kSlots) {
+      const int rc = launch_held(c);
+      if (rc) return rc;
+    }
     if (pending_jobs(c) >= kSlots * c->merge || c->held == c->merge)
       return set_err(MJG_E_STATE, "%d submits queued: sync one first", pending_jobs(c));
     c->held_p[c->held] = frames;

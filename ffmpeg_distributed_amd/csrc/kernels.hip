@@ -36,8 +36,7 @@ constexpr int kSlotWords = (64 * kMaxBlockBits + 31) / 32;  // one chunk = 64 bl
 // The row image (s_pk) holds row-pass output 0 (the row sum, 0..32640) unbiased and outputs
 // 1-7 (|value| <= 16320) + 16384, so every u16 is below 2^15 and reads as the same value
 // when v_dot2_i32_i16 takes it as int16 (exact_coef: no sign fix-up).
-constexpr int kMfTabOff = 704;   // MF k_encode's f16 MFMA fragments (open_ctx, dct_mfma)
-constexpr int kTabWords = kMfTabOff + 12 * 64 * 4;  // device table block, see open_ctx
+constexpr int kTabWords = 704;  // device table block, see open_ctx
 constexpr float kM = 12582912.0f;
 constexpr float kMc = 12599296.0f;  // kM + 16384: the row image's bias for outputs 1-7
 constexpr float kRnd = 0x1p-10f;
@@ -717,11 +716,9 @@ __device__ __forceinline__ void task_pos(const EncGeom &g, int t, int &frame, in
   bbase = (seg - frame * g.nseg) * g.seg_blocks;
 }
 
-// chunks per work unit pulled from the counters: 12 for the VALU DCT stage (with the per-XCD
-// counters: c2 -6%, c5 -5% against 16; 8 and 24 measured too), 8 for the MFMA stage (3 waves
-// per SIMD, fewer chunks per wave), each the faster on its BASELINE configs
-template <bool MF>
-constexpr int kBatchOf = MF ? 8 : 12;
+// chunks per work unit pulled from the counters: 12 (with the per-XCD counters: c2 -6%, c5 -5%
+// against 16; 8 and 24 measured too)
+constexpr int kBatch = 12;
 
 // DC predictor carried into a chunk that does not follow this wave's previous chunk: the
 // quantised DCs of the 8 blocks before it (every possible predecessor: distance <= 8),
@@ -1059,173 +1056,6 @@ __device__ __forceinline__ int dc_predictor(int dc, int carry, int delta, bool f
   return lane >= delta ? from_cur : (first_chunk ? 128 : from_prev);
 }
 
-// ------------------------------------------------ DCT on the matrix cores (MF k_encode)
-// Both jfdctint passes of a chunk as v_mfma_f32_32x32x16_f16 products, 32 blocks (one
-// "group", blocks 32g .. 32g+31 of the chunk) per MFMA column set:
-//
-//   pass 1, exact: D_t[n][blk] = sum_k A1[n][k] * P[k][blk], n = (row r_loc, output i) for
-//     pixel rows 4t .. 4t+3, k = (row, x) of two pixel rows per K-step.  P = pixel - 128 in
-//     f16 (exact); A1 = the LLM butterfly multiplied out (kPass2Dot rows; rows 0/4: +-16),
-//     split into two f16 digits (c = 64 round(c/64) + rest), both exact, divided by 512 where
-//     FFmpeg descales by 9 (a power of two: still exact).  Every partial sum is a multiple of
-//     2^-10 below 2^14 (|sum| <= 128 * 59642 / 512), so the f32 accumulation is exact in any
-//     order; the accumulator starts at 2^-10 (0 for outputs 0/4), so adding M' = 1.5 2^23 +
-//     16384 rounds to FFmpeg's DESCALE and leaves y + 16384 in the low mantissa bits, the u16
-//     row image s_pk of the VALU row pass.  Centring moves only the row sums (output 0) by a
-//     constant, which every AC row of pass 2 cancels (its coefficients sum to 0); centred,
-//     they too fit 0..32767 with the +16384 (exact_coef never reads column 0's row 0).
-//   pass 2, a screen: Z_t[z][blk] = sum_k A2[z][k] * f16(D)[k][blk] with A2 = pass-2 rows
-//     scaled by 2^10 / tau_z, tau_z = the quantiser threshold of zigzag coefficient z minus
-//     the f16 rounding bound (open_ctx): |Z| > 2^10 whenever the coefficient quantises to
-//     nonzero.  D's accumulator registers are the B operand directly (rows of D = K, no lane
-//     movement).  Row order of A2: lane half h, register q of Z_t holds zigzag 32h + 31 - 16t
-//     - q, so the candidate word shifted together in processing order is the zigzag mask
-//     (bits 32h .. 32h+31 of the block).  z = 0 is the exact column sum (A2 = 1): the DC.
-//
-// Operand maps (gfx950, f16 32x32x16): lane l holds A[l & 31][8 (l >> 5) + j] and
-// B[8 (l >> 5) + j][l & 31] in element j, C/D[(q & 3) + 8 (q >> 2) + 4 (l >> 5)][l & 31] in
-// register q.  Lane = block in the rest of k_encode; permlane32_swap moves the odd pixel
-// rows of blocks 0-31 and the even rows of blocks 32-63 across (group g's lane l then holds
-// rows 2s + (l >> 5) of block 32g + (l & 31)), and moves the masks / DCs back.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-// tabs[kMfTabOff..]: A1 = 4 fragments (P0 hi, P0 lo, P1 hi, P1 lo), A2 = 8 ([t][s']), [frag][lane] uint4
-constexpr float kScr2 = 1048576.0f;       // (2^10)^2: screen threshold on Z^2
-
-__device__ __forceinline__ uint32_t f16x2_bits(f16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-
-// 8 pixels of a row (two little-endian words) -> 8 f16 (p - 128), exact.  The byte goes
-// into the mantissa of f16 1024 (0x64 high byte): f16 1024 + p, then one packed subtract.
-// RC: each byte through swscale's tv->pc table first (d16 loads fill the u16 halves).
-template <bool RC>
-__device__ __forceinline__ uint4 pix_frag(uint32_t lo, uint32_t hi, int tab, const uint8_t *s_rc) {
-  uint32_t w[4];
-  if (RC) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t src = k < 2 ? lo : hi;
-      const uint32_t a0 = __builtin_amdgcn_perm((uint32_t)tab, src, 0x0c0c0400u | (uint32_t)(2 * (k & 1)));
-      const uint32_t a1 = __builtin_amdgcn_perm((uint32_t)tab, src, 0x0c0c0400u | (uint32_t)(2 * (k & 1) + 1));
-      w[k] = ((uint32_t)s_rc[a0] | ((uint32_t)s_rc[a1] << 16)) | 0x64006400u;
-    }
-  } else {
-    w[0] = __builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u);
-    w[1] = __builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u);
-    w[2] = __builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u);
-    w[3] = __builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u);
-  }
-  const f16x2 off = {(_Float16)-1152.0f, (_Float16)-1152.0f};
-  uint4 r;
-  r.x = f16x2_bits(__builtin_bit_cast(f16x2, w[0]) + off);
-  r.y = f16x2_bits(__builtin_bit_cast(f16x2, w[1]) + off);
-  r.z = f16x2_bits(__builtin_bit_cast(f16x2, w[2]) + off);
-  r.w = f16x2_bits(__builtin_bit_cast(f16x2, w[3]) + off);
-  return r;
-}
-
-__device__ __forceinline__ f32x16 mfma16(uint4 a, uint4 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
-                                                 0);
-}
-
-// One group: rows[s] = (lo, hi) words of pixel row 2s + (lane >> 5) of block 32g + (lane & 31).
-// Writes the group's 32 columns of s_pk; returns the candidate word (zigzag 32h .. 32h+31,
-// MSB first) and, in lanes 0-31, the DC column sum.
-template <bool RC>
-__device__ __forceinline__ uint32_t dct_group(const uint32_t (&rows)[4][2], int tab, const uint8_t *s_rc,
-                                              const uint4 *s_f, uint32_t *s_pk, int g, int lane, float &dcz) {
-  asm volatile("" ::: "memory");  // fragments re-read from LDS per group, not held in registers
-  uint4 bp[4];
-#pragma unroll
-  for (int s = 0; s < 4; s++) bp[s] = pix_frag<RC>(rows[s][0], rows[s][1], tab, s_rc);
-  // pattern P1 (output row r_loc = 2 + h) is P0 (r_loc = h) moved by 16 lanes: lane l ^ 16
-  const uint4 p0h = s_f[0 * 64 + lane], p0l = s_f[1 * 64 + lane], p1h = s_f[0 * 64 + (lane ^ 16)],
-              p1l = s_f[1 * 64 + (lane ^ 16)];
-  f32x16 d[2];
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-#pragma unroll
-    for (int q = 0; q < 16; q++) d[t][q] = (q & 3) ? kRnd : 0.0f;
-    d[t] = mfma16(p0h, bp[2 * t], d[t]);
-    d[t] = mfma16(p0l, bp[2 * t], d[t]);
-    d[t] = mfma16(p1h, bp[2 * t + 1], d[t]);
-    d[t] = mfma16(p1l, bp[2 * t + 1], d[t]);
-  }
-  // s_pk: word (i * 4 + r / 2) of block 32g + (lane & 31); this lane holds outputs
-  // i = 4h .. 4h+3 of rows 4t .. 4t+3 (register q: row 4t + q / 4, output 4h + q % 4)
-  uint32_t *pk = s_pk + (lane >> 5) * 16 * 64 + g * 32 + (lane & 31);
-  uint4 b2[4];
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-#pragma unroll
-    for (int q = 0; q < 16; q = (q & 3) == 3 ? q + 5 : q + 1) {  // q = 0-3, 8-11: rows 4t + 2 (q >> 3), + 1
-      // + 16384 on every output: the centred row sums (-16384..16256) included
-      const uint32_t o0 = __float_as_uint(d[t][q] + kMc), o1 = __float_as_uint(d[t][q + 4] + kMc);
-      pk[((q & 3) * 4 + 2 * t + (q >> 3)) * 64] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      uint32_t v[4];
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const f16x2 hv = {(_Float16)d[t][8 * s + 2 * e], (_Float16)d[t][8 * s + 2 * e + 1]};
-        v[e] = f16x2_bits(hv);
-      }
-      b2[2 * t + s] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-  }
-  uint32_t w = 0;
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-    f32x16 z;
-#pragma unroll
-    for (int q = 0; q < 16; q++) z[q] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 4; s++) z = mfma16(s_f[(4 + 4 * t + s) * 64 + lane], b2[s], z);
-#pragma unroll
-    for (int q = 0; q < 16; q++)
-      w = __builtin_amdgcn_alignbit(w, __float_as_uint(__builtin_fmaf(-z[q], z[q], kScr2)), 31);
-    if (t == 1) dcz = z[15];
-  }
-  return w;
-}
-
-template <typename T>
-__device__ __forceinline__ void swap32(T &a, T &b) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
-                                                  false, false);
-  a = __builtin_bit_cast(T, (uint32_t)r[0]);
-  b = __builtin_bit_cast(T, (uint32_t)r[1]);
-}
-
-// The chunk's DCT on the matrix cores: raw rows of this lane's block in, s_pk written, the
-// exact quantised DC and the zigzag candidate mask (DC bit clear) of this lane's block out.
-template <bool RC>
-__device__ __forceinline__ uint64_t dct_mfma(const uint64_t (&raw)[8], int tab, const uint8_t *s_rc, const uint4 *s_f,
-                                             uint32_t *s_pk, int lane, int &dc) {
-  uint32_t rg[2][4][2];  // [group][K-step][word]
-#pragma unroll
-  for (int s = 0; s < 4; s++)
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      uint32_t e = (uint32_t)(raw[2 * s] >> (32 * k)), o = (uint32_t)(raw[2 * s + 1] >> (32 * k));
-      swap32(e, o);  // e: rows 2s + h of blocks 0-31; o: of blocks 32-63
-      rg[0][s][k] = e;
-      rg[1][s][k] = o;
-    }
-  int tab0 = tab, tab1 = tab;
-  if (RC) swap32(tab0, tab1);  // lane l: the tables of blocks l & 31 and 32 + (l & 31)
-  float dz0, dz1;
-  uint32_t w0 = dct_group<RC>(rg[0], tab0, s_rc, s_f, s_pk, 0, lane, dz0);
-  uint32_t w1 = dct_group<RC>(rg[1], tab1, s_rc, s_f, s_pk, 1, lane, dz1);
-  swap32(w0, w1);    // lane = block: w0 zigzag 0-31, w1 zigzag 32-63
-  swap32(dz0, dz1);  // lane = block: dz0 its DC column sum
-  // quantised DC = floor((sum + 520) / 1024) with sum = dz0 + 8 * 16384 (centring), exact
-  dc = (int)(__float_as_uint(__builtin_fmaf(dz0, 1.0f / 1024, 128.0f + 0x1.1p-7f) + kM) - 0x4B400000u);
-  return (((uint64_t)w1 << 32) | w0) & ~1ull;
-}
-
 // k_encode's work units per XCD: workgroup i runs on XCD i % 8 (round-robin dispatch), and
 // XCD j's waves take the units of the j-th eighth of the launch first (its own counter,
 // work_ctr[j * kCtrStride]: neighbouring chunks share the 64-byte sectors at their edges, so
@@ -1251,10 +1081,11 @@ struct XcdUnits {
   }
 };
 
-// MF: the DCT stage on the matrix cores (dct_mfma) instead of row_pass + column_screen.
 // DBG: the MJG_F_DEBUG_COEFS instantiation (quantised blocks out); the product kernels carry
 // neither its branch nor its live scalars (k_encode is short of SGPRs: they spill to VGPR lanes).
-template <bool RC, int MODE, bool MF = false, bool DBG = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
+// (The DCT stage on the matrix cores, dct_mfma, r02-r05, was retired in r06: slower or equal on
+// every BASELINE config once the VALU screen skipped columns, profiles/HISTORY.md §4c.)
+template <bool RC, int MODE, bool DBG = false>  // RC: yuv420p (tv) input without scale -> swscale tv->pc per pixel
 __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPerEU) void k_encode(
     const SegList frames, EncGeom g, const uint32_t *__restrict__ tabs,
     uint32_t *__restrict__ scratch, uint32_t *__restrict__ chunk_bits,
@@ -1267,14 +1098,12 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
   __shared__ __attribute__((aligned(16))) int32_t s_qc[64];  // qmat column-major: [col][row]
   __shared__ uint8_t s_zz[64];                                // zigzag -> natural index
   __shared__ uint4 s_zd[64];                                  // zigzag -> exact_coef descriptor (zz_desc)
-  constexpr bool SCR = !MF;  // the VALU column screen
-  __shared__ __attribute__((aligned(16))) float s_thr[SCR ? 64 : 4];  // screening thresholds^2 [col][row]
+  __shared__ __attribute__((aligned(16))) float s_thr[64];  // screening thresholds^2 [col][row]
   __shared__ __attribute__((aligned(16))) uint32_t s_m2[32];  // pass-2 dot rows as int16 pairs
   __shared__ uint8_t s_rc[RC ? 512 : 1];  // tv->pc: luma [0,256), chroma [256,512)
-  __shared__ uint4 s_f[MF ? 12 * 64 : 1];  // MFMA A fragments (dct_mfma): [0, 2) pass 1, [4, 12) pass 2
   __shared__ uint32_t s_desc[8];                   // block-of-MCU descriptors (EncGeom)
   __shared__ uint4 s_bd[16];                       // their plane fields (BlockDesc)
-  __shared__ uint32_t s_skip[SCR ? 12 : 1];        // column-skip limits, 3 u16x2 words per pair
+  __shared__ uint32_t s_skip[12];        // column-skip limits, 3 u16x2 words per pair
   __shared__ uint32_t s_pk_all[kWavesPerWg][32 * 64];  // quantised blocks, [word][lane]
   // emit_block_wave's stream words, pack_chunk_short's chunk words
   __shared__ uint32_t s_hv_all[MODE == kEmitDefault ? kWavesPerWg : 1][kHvWords];
@@ -1290,7 +1119,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
     s_qc[tid] = (int32_t)tabs[544 + tid];
     s_zz[tid] = kZigzag[tid];
     s_zd[tid] = zz_desc(tid, tabs);
-    if (SCR) s_thr[tid] = __uint_as_float(tabs[608 + tid]);
+    s_thr[tid] = __uint_as_float(tabs[608 + tid]);
     if (tid < 32)
       s_m2[tid] = pass2_pair(tid);
   }
@@ -1298,9 +1127,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
     s_desc[tid] = tabs[672 + tid];
   }
   init_block_desc(g, tabs, s_bd, tid);
-  if (SCR && tid < 12) s_skip[tid] = tabs[680 + tid];
-  if (MF)
-    for (int i = tid; i < 12 * 64; i += 64 * kWavesPerWg) s_f[i] = ((const uint4 *)(tabs + kMfTabOff))[i];
+  if (tid < 12) s_skip[tid] = tabs[680 + tid];
   if (RC)
     for (int i = tid; i < 512; i += 64 * kWavesPerWg)
       s_rc[i] = (uint8_t)(i < 256 ? range_luma(i) : range_chroma(i - 256));
@@ -1316,7 +1143,6 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
   __syncthreads();  // tables visible; the only workgroup barrier
 
   const int gw = blockIdx.x * kWavesPerWg + wave;
-  constexpr int kBatch = kBatchOf<MF>;
   const int nbatch = (ntasks + kBatch - 1) / kBatch;
   constexpr int NX = MODE == kEmitDefault ? kXcds : 1;
   const XcdUnits<NX> xu{(int)(blockIdx.x & (NX - 1)), nbatch};
@@ -1357,11 +1183,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
     const int tab = desc_tab(dsc);
     if (active && !fast) fetch_rows_edge(raw, fb, block_pos(g, bbase + b, s_bd));
     int dc = 0;
-    uint64_t mask = 0;
-    if (MF)
-      mask = dct_mfma<RC>(raw, tab, s_rc, s_f, s_pk, lane, dc);
-    else
-      row_pass<RC>(raw, tab, s_rc, s_pk, lane);
+    row_pass<RC>(raw, tab, s_rc, s_pk, lane);
     // prefetch the next chunk while this one is encoded
     const int cur_frame = frame, cur_chunk = chunk, cur_bbase = bbase;
     const bool cur_active = active;
@@ -1383,7 +1205,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
 
     uint32_t mlo = 0, mhi = 0;  // candidate mask, scan positions 0-31 / 32-63 (column_screen)
     if (cur_active) {
-      if (SCR) column_screen(s_pk, lane, s_skip, s_thr, dc, mlo, mhi, skip_st, (t & 3) == 0);
+      column_screen(s_pk, lane, s_skip, s_thr, dc, mlo, mhi, skip_st, (t & 3) == 0);
       if (DBG && g.debug_coefs) {  // natural-order int16 pairs of the exact quantised block
         uint32_t *dst = (uint32_t *)(dbg_coefs +
                                      ((size_t)cur_frame * g.nmcu * g.bpm + cur_bbase + cur_chunk * 64 + lane) * 64);
@@ -1395,7 +1217,7 @@ __global__ __launch_bounds__(64 * kWavesPerWg, MODE == kCount ? 4 : kEncWavesPer
         }
       }
     }
-    if (SCR) mask = ((uint64_t)mhi << 32) | mlo;
+    const uint64_t mask = ((uint64_t)mhi << 32) | mlo;
 
     // DC predictor (FFmpeg last_dc, 128 at every segment start): shuffle within the chunk,
     // else the carried DCs of the previous chunk.

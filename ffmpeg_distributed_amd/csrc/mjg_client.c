@@ -102,7 +102,10 @@ static int sock_name(const char *dev, const char *pkg, char *name, size_t cap) {
   h = fnv(h, ml);
   h = fnv(h, getenv("MJG_NUMA_BIND"));
   h = fnv(h, getenv("MJG_SERVE_BATCH_BYTES"));
-  h = fnv(h, getenv("MJG_MERGE"));  // read once by the library at mjg_open
+  // read by the library at mjg_open, in the encoder's process
+  h = fnv(h, getenv("MJG_MERGE"));
+  h = fnv(h, getenv("MJG_MERGE_HOLD"));
+  h = fnv(h, getenv("MJG_TIMING_NOTAIL"));
   h = fnv(h, kMagic);  // the protocol: a client never meets an encoder of another wire format
   snprintf(name, cap, "mjg-gpu-%u-%s-%llx-%llx-%llx", (unsigned)getuid(), dev, (unsigned long long)st.st_ino,
            (unsigned long long)st.st_mtim.tv_sec * 1000000000ull + (unsigned long long)st.st_mtim.tv_nsec,

@@ -56,7 +56,7 @@ class MjpegEncoder:
                  sar=(1, 1), max_batch: int = 16, timing: bool = False,
                  debug_coefs: bool = False, sws_bitexact: bool = True, com_itu601: bool = False,
                  huffman: str = "default", chroma: str = "420", rst: bool = False,
-                 dct_mfma: Optional[bool] = None, merge: bool = True):
+                 merge: bool = False):
         self._L = _lib.load()
         self.device = int(device)
         self.src_w, self.src_h = int(src_w), int(src_h)
@@ -80,16 +80,11 @@ class MjpegEncoder:
             raise ValueError(f"huffman {huffman!r}")
         if rst:
             flags |= _lib.MJG_F_RST
-        # k_encode's DCT stage: None = the library's choice (the VALU passes),
-        # True = the matrix cores, False = the VALU passes
-        if dct_mfma is True:
-            flags |= _lib.MJG_F_DCT_MFMA
-        elif dct_mfma is False:
-            flags |= _lib.MJG_F_DCT_VALU
-        # library-side merging of single-segment device submits (mjg_submit); merge=False: every
-        # submit is a launch of its own
-        if not merge:
-            flags |= _lib.MJG_F_NO_MERGE
+        # library-side merging of single-segment device submits (MJG_F_MERGE, opt-in): a device
+        # submit is held and launched with the next one, so its frames must stay unchanged until
+        # its own sync; merge=False: every submit is a launch of its own, launched in submit()
+        if merge:
+            flags |= _lib.MJG_F_MERGE
         self.huffman = huffman
         self.chroma = str(chroma)
         if self.chroma not in _lib.CHROMA_FORMATS:
@@ -146,7 +141,8 @@ class MjpegEncoder:
     @property
     def depth(self) -> int:
         """Device-pointer submits (submit(device_ptr=...)) pending at most before one must be
-        synced (mjg_ctx_queue_depth: two launches of up to two merged submits)."""
+        synced (mjg_ctx_queue_depth: two launches, of up to two merged submits each with
+        merge=True)."""
         if hasattr(self._L, "mjg_ctx_queue_depth"):
             return int(self._L.mjg_ctx_queue_depth(self._h))
         return self.host_depth
@@ -161,8 +157,8 @@ class MjpegEncoder:
         """Queue `nframes` packed frames: a host buffer (numpy / bytes) or a device pointer
         (`device_ptr`, e.g. torch_tensor.data_ptr() on this GPU, kept alive until its sync).
         Up to `host_depth` host submits may be queued (each one's k_encode runs beside the
-        previous one's drain and tail kernels), up to `depth` device submits: the library
-        holds a device submit while a launch is queued and launches it with the next one."""
+        previous one's drain and tail kernels), up to `depth` device submits: with merge=True the
+        library holds a device submit and launches it with the next one."""
         if device_ptr is not None:
             if nframes is None:
                 raise ValueError("nframes is required with device_ptr")

@@ -637,16 +637,23 @@ def run(device: int, args: List[str], stdin=None, stdout=None, stderr=None, cach
             src.close(kill=True)
             th.join(timeout=5.0)
         stuck = th.is_alive()  # blocked on a stdin pipe that never delivers: leak, never free
+        # the muxer's packets are views into the page-locked output buffers: one still inside
+        # a write (a stdout pipe that does not drain) keeps them, so they are leaked, not freed
+        mux_stuck = mt.is_alive()
         rc = src.close(kill=failed)
-        if (failed or stuck) and cache is not None:  # a submit may still be queued: start afresh
+        if (failed or stuck or mux_stuck) and cache is not None:  # a submit may still be queued: start afresh
             for k in ("key", "enc", "bufs", "obufs"):
                 cache.pop(k, None)
             cache = None
         if cache is None:
             enc.close()
             if not stuck:
-                for b in bufs + [b for b in obufs if b is not None]:
+                for b in bufs:
                     b.free()
+            if not mux_stuck:
+                for b in obufs:
+                    if b is not None:
+                        b.free()
     if rc:
         stderr.write(f"decoder exited with {rc}\n")
         return 1

@@ -61,20 +61,10 @@ extern "C" {
 #define MJG_F_TIMING_DETAIL 64u /* MJG_F_TIMING plus events around every tail kernel (scan, 0xFF
                                   count, write: MJG_K_SCAN_BITS .. MJG_K_WRITE); each event adds
                                   ~10 us of GPU idle between those short kernels */
-#define MJG_F_FUSED 128u       /* retired (r05): the one-kernel scale + encode (k_scale_encode)
-                                  measured slower than k_scale + k_encode on MI355X and left the
-                                  library; the flag is accepted and ignored
-                                  (the bytes never depended on it) */
-
-#define MJG_F_DCT_MFMA 256u    /* -huffman default: k_encode's two jfdctint passes on the matrix cores
-                                  (v_mfma_f32_32x32x16_f16: pass 1 exact in two f16 digits, pass 2
-                                  a quantiser screen), dct_mfma in kernels.hip.  Same bytes.  Opt-in
-                                  (the default with -vf scale until r05, now measured slower or
-                                  equal there too: DESIGN.md section 4.3) */
-#define MJG_F_DCT_VALU 512u    /* -huffman default: the VALU passes (the default; overrides DCT_MFMA) */
-#define MJG_F_NO_MERGE 1024u   /* no library-side merging: every mjg_submit is a launch of its own
-                                  (by default single-segment device submits are held while the GPU
-                                  has a launch queued and launched two at a time, see mjg_submit) */
+#define MJG_F_MERGE 1024u      /* opt-in library-side merging: single-segment device submits are held
+                                  and launched two at a time (see mjg_submit; the caller keeps each
+                                  submit's frames valid until its own mjg_sync).  Without it every
+                                  mjg_submit is a launch of its own, launched inside the call */
 
 /* Kernel ids for mjg_kernel_times() */
 #define MJG_K_SCALE 0          /* bicubic hscale + range + vscale (per plane) */
@@ -131,13 +121,15 @@ int mjg_header(const mjg_ctx *ctx, uint8_t *out, size_t cap, size_t *len);
  * previous one's drain and tail.  src_is_device = 0: `frames` is host memory (copied H2D
  * through the slot's staging buffer; pinned memory from mjg_host_alloc() makes this
  * asynchronous), a launch of its own; src_is_device = 1: `frames` is device memory on ctx's
- * device, read in place.  Library-side merging (unless MJG_F_NO_MERGE / MJG_MERGE=1): a
- * device submit made while a launch is queued is held and launched together with the next
- * device submit, as one segment list (mjg_submit_segments' kernels), or alone when the GPU
- * runs dry or the caller syncs it; each submit stays a job of its own for mjg_sync / mjg_fetch
- * with exactly the bytes of an unmerged launch.  The frames must stay valid until the job is
- * synced.  Up to mjg_ctx_queue_depth(ctx) device submits may be pending; MJG_E_STATE past
- * that (or when no launch slot is free for a host submit).
+ * device, read in place.  Without MJG_F_MERGE every submit is launched (stream-ordered) inside
+ * this call.  With MJG_F_MERGE (opt-in; MJG_MERGE=1 in the environment turns it off again) a
+ * device submit is held and launched together with the next device submit, as one segment
+ * list (mjg_submit_segments' kernels), or alone when the caller syncs it; each submit stays a
+ * job of its own for mjg_sync / mjg_fetch with exactly the bytes of an unmerged launch.  A held
+ * submit's kernels read its frames after this call returns, so with MJG_F_MERGE the frames must
+ * stay valid and unchanged until the job is synced (stream order on the caller's side does not
+ * protect them).  Up to mjg_ctx_queue_depth(ctx) device submits may be pending; MJG_E_STATE
+ * past that (or when no launch slot is free for a host submit).
  * Replaces the per-segment encode the reference runs at ffmpeg_distributed.py:139-141. */
 int mjg_submit(mjg_ctx *ctx, const uint8_t *frames, int nframes, int src_is_device);
 /* Several segments in one submit: segment k's seg_nframes[k] packed I420 frames at device
@@ -176,8 +168,8 @@ void *mjg_stream(mjg_ctx *ctx);
  * and mjg_submit_segments, which each take a launch of their own. */
 int mjg_queue_depth(void);
 /* How many single-segment device submits (mjg_submit, src_is_device = 1) ctx holds pending
- * before one must be synced: mjg_queue_depth() launches of up to two merged submits each (4),
- * or mjg_queue_depth() when merging is off. */
+ * before one must be synced: with MJG_F_MERGE mjg_queue_depth() launches of up to two merged
+ * submits each (4), else mjg_queue_depth(). */
 int mjg_ctx_queue_depth(const mjg_ctx *ctx);
 
 /* Pinned host memory for mjg_submit / mjg_fetch. */

@@ -337,7 +337,7 @@ def test_4k_segment_batch_from_device_memory():
     torch.cuda.synchronize()
     host = pool.cpu().numpy()
     assert (host[59] == make_testsrc(w, h, 1059)).all()  # the device generator = the host one
-    with MjpegEncoder(0, w, h, qscale=5, max_batch=n) as enc:
+    with MjpegEncoder(0, w, h, qscale=5, max_batch=n, merge=True) as enc:
         enc.submit(device_ptr=pool.data_ptr(), nframes=n)
         enc.submit(device_ptr=pool[60].data_ptr(), nframes=60)
         s0 = enc.sync()
@@ -575,7 +575,7 @@ def test_pipelined_submits():
     frames = rand_frames(w, h, 7, seed=21, kind="smooth")
     ref = oracle_frames(frames, w, h, q, False)
     with MjpegEncoder(0, w, h, qscale=q, max_batch=3) as enc:
-        assert enc.host_depth == 2 and enc.depth == 4  # host submits: one launch each
+        assert enc.host_depth == 2 and enc.depth == 2  # host submits: one launch each
         enc.submit(frames[0:3])
         enc.submit(frames[3:5])
         with pytest.raises(MjgError):
@@ -706,6 +706,40 @@ def test_merged_4k_segments_equal_unmerged():
     assert res[True][0] == res[False][0]
 
 
+@pytest.mark.parametrize("depth", [3, 4])
+def test_merge_depth_env_keeps_queue_depth(depth, monkeypatch):
+    """MJG_MERGE=3 / 4 (jobs per merged launch, an A/B switch read at mjg_open): 23 ragged device
+    submits in the bench's pattern (sync when enc.depth are pending) and in an eager pattern
+    (sync after every second submit), never refused while fewer than enc.depth are pending (a
+    full held group waiting at mjg_sync is launched by the next submit), every job's
+    JPEGs byte-equal to the oracle."""
+    import torch
+    monkeypatch.setenv("MJG_MERGE", str(depth))
+    w, h = 72, 40
+    counts = [1 + (7 * j) % 3 for j in range(23)]
+    frames = rand_frames(w, h, sum(counts), seed=505, kind="testsrc")
+    ref = oracle_frames(frames, w, h, 4, False)
+    dev_frames = torch.from_numpy(frames.copy()).to("cuda:0")
+    torch.cuda.synchronize()
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    fb = frames.shape[1]
+    for eager in (False, True):
+        got = []
+        with MjpegEncoder(0, w, h, qscale=4, max_batch=3, merge=True) as enc:
+            assert enc.depth == 2 * depth
+            for j, k in enumerate(counts):
+                enc.submit(device_ptr=dev_frames.data_ptr() + int(offs[j]) * fb, nframes=k)
+                if enc.pending == enc.depth or (eager and j % 2 == 1):
+                    enc.sync()
+                    got += enc.fetch()
+            while enc.pending:
+                enc.sync()
+                got += enc.fetch()
+        assert len(got) == len(ref)
+        for i in range(len(ref)):
+            assert got[i] == ref[i], (depth, eager, i, first_diff(got[i], ref[i]))
+
+
 @pytest.mark.parametrize("cfg", ["optimal", "scale", "scale_optimal", "default"])
 def test_pipelined_submits_two_streams(cfg):
     """Every context runs its two slots on two streams (consecutive submits' launches overlap,
@@ -832,45 +866,12 @@ def test_wave_parallel_blocks_match_oracle(q, full, huffman):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
-# ------------------------------------------- k_encode's DCT on the matrix cores (MJG_F_DCT_MFMA)
-# dct_mfma: pass 1 exact in two f16 digits, pass 2 a quantiser screen whose candidates are
-# quantised exactly (the same bytes), the permlane32 exchange and the zigzag mask.
-
-@pytest.mark.parametrize("mode", [True, False])
-@pytest.mark.parametrize("part", range(4))
-def test_dct_mfma_random_sweep(part, mode):
-    """Every -huffman default case of the 600-case random sweep (sizes, q 1..31, tv/pc,
-    six contents, 4:2:0/4:2:2/4:4:4, RST, scaling, ragged batches) with k_encode's DCT stage
-    forced onto the matrix cores (True) or the VALU (False; the library's default picks
-    the matrix cores for scaled input and the VALU otherwise, which the plain sweep covers)."""
-    _sweep([c for c in SWEEP if c["huffman"] == "default"][part::4], dct_mfma=mode)
-
-
-@pytest.mark.parametrize("mode", [True, False])
-def test_dct_mfma_large_sweep(mode):
-    _sweep([c for c in SWEEP_LARGE if c["huffman"] == "default"], dct_mfma=mode)
-
-
-@pytest.mark.parametrize("mode", [True, False])
-@pytest.mark.parametrize("w,h,q", [(72, 40, 5), (1920, 1080, 3)])
-def test_dct_mfma_coefficients(w, h, q, mode):
-    frames = rand_frames(w, h, 2, seed=1, kind="smooth" if w < 200 else "testsrc")
-    with MjpegEncoder(0, w, h, qscale=q, full_range=True, max_batch=2, debug_coefs=True,
-                      dct_mfma=mode) as enc:
-        enc.submit(frames)
-        enc.sync()
-        for i in range(2):
-            y, u, v = split_i420(frames[i], w, h)
-            ref, _ = oracle.frame_coeffs(y, u, v, q)
-            bad = np.nonzero((enc.debug_coefs(i) != ref).any(1))[0]
-            assert bad.size == 0, (i, bad[:10])
-
-
-@pytest.mark.parametrize("mode", [True, False])
+# ------------------------------------------- extreme blocks at the quantiser's ends
 @pytest.mark.parametrize("q,full", [(1, False), (31, True)])
-def test_dct_mfma_extremes(q, full, mode):
-    """Extreme blocks for the screen's error bound: full-swing checkers (pass-1 outputs
-    near 2^14), black/white blocks, noise, at the finest and coarsest quantiser."""
+def test_extreme_blocks(q, full):
+    """Extreme blocks for the fp32 row pass and the column screen's margins: full-swing
+    checkers (row-pass outputs near 2^14), black/white blocks, noise, at the finest and
+    coarsest quantiser."""
     w, h = 256, 128
     rng = np.random.default_rng(q)
     y = np.where((np.arange(w)[None, :] // 1 + np.arange(h)[:, None]) % 2, 255, 0).astype(np.uint8)
@@ -881,30 +882,9 @@ def test_dct_mfma_extremes(q, full, mode):
     u = rng.integers(0, 256, (h // 2, w // 2)).astype(np.uint8)
     v = np.where(np.arange(w // 2)[None, :] % 2, 0, 255).repeat(h // 2, 0).astype(np.uint8)
     frames = np.stack([pack_i420(y, u, v)])
-    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=1, dct_mfma=mode) as enc:
+    with MjpegEncoder(0, w, h, qscale=q, full_range=full, max_batch=1) as enc:
         got = enc.encode(frames)
     assert got[0] == oracle_frames(frames, w, h, q, full)[0]
-
-
-def test_dct_mfma_4k_segment_from_device_memory():
-    """BASELINE configs[1] as the bench submits it, through the MFMA DCT: a 120-frame 4K
-    segment by device pointer, every frame byte-equal to the oracle."""
-    import torch
-    from ffmpeg_distributed_amd.testsrc import testsrc2_i420_torch
-    w, h, n = 3840, 2160, 120
-    dev = torch.device("cuda", 0)
-    pool = torch.empty((n, i420_frame_bytes(w, h)), dtype=torch.uint8, device=dev)
-    for i in range(0, n, 20):
-        pool[i:i + 20] = testsrc2_i420_torch(w, h, 2000 + i, 20, dev)
-    torch.cuda.synchronize()
-    host = pool.cpu().numpy()
-    with MjpegEncoder(0, w, h, qscale=5, max_batch=n, dct_mfma=True) as enc:
-        enc.submit(device_ptr=pool.data_ptr(), nframes=n)
-        enc.sync()
-        a = enc.fetch()
-    ref = _oracle_many(host, w, h, qscale=5)
-    for i in range(n):
-        assert a[i] == ref[i], (i, len(a[i]), len(ref[i]), first_diff(a[i], ref[i]))
 
 
 # ------------------------------------------- a long -huffman optimal launch

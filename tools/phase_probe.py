@@ -35,8 +35,7 @@ def main():
         _lib._lib = None
         _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
         from ffmpeg_distributed_amd.encoder import MjpegEncoder
-        enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, huffman="default",
-                           dct_mfma=False)
+        enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, huffman="default")
         L = _lib.load()
         L.mjg_probe_phase.argtypes = [C.POINTER(C.c_ulonglong)]
         acc = (C.c_ulonglong * 8)()

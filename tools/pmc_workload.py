@@ -15,7 +15,6 @@ def main():
     p.add_argument("--workload", default="c2")
     p.add_argument("--content", default="testsrc")
     p.add_argument("--launches", type=int, default=3)
-    p.add_argument("--dct", choices=["auto", "mfma", "valu"], default="auto", help="k_encode's DCT stage")
     a = p.parse_args()
     import torch
     import bench
@@ -30,8 +29,7 @@ def main():
         k = min(10, SEG - i)
         pool[i:i + k] = gen(W, H, i, k, dev, full_range=FULL)
     torch.cuda.synchronize()
-    enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF,
-                       dct_mfma={"auto": None, "mfma": True, "valu": False}[a.dct])
+    enc = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=SEG, huffman=HUFF)
     tot = 0
     for _ in range(a.launches):
         enc.submit(device_ptr=pool.data_ptr(), nframes=SEG)

@@ -64,10 +64,8 @@ def main():
         _lib._lib = None
         _lib.LIB_PATH = os.path.join(ROOT, "ffmpeg_distributed_amd", f"libmjgpu_v_{name}.so")
         from ffmpeg_distributed_amd.encoder import MjpegEncoder
-        # a name ending in "_m" / "_v" forces k_encode's DCT stage onto the matrix cores / the VALU
         encs[name] = MjpegEncoder(0, W, H, DW, DH, full_range=FULL, qscale=Q, max_batch=N, timing=True,
-                                  huffman=HUFF,
-                                  dct_mfma=True if name.endswith("_m") else False if name.endswith("_v") else None)
+                                  huffman=HUFF)
     res = {n: [] for n in encs}
     ref = None
     names = list(encs)
