@@ -424,7 +424,7 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
     }
     if (ok) {
       const int d = p.hf.pos[xa] & 3;
-      std::vector<int32_t> mfb(64 * 8, 0);
+      std::vector<int32_t> mfb(kMvFragOff + 3 * 64 * 4, 0);
       for (int l = 0; l < 64; l++)
         for (int j = 0; j < 16; j++) {
           const int k = 16 * (l >> 4) + j, n = l & 15, t = k - 2 * n - d;
@@ -434,6 +434,40 @@ int setup_plane_scale(mjg_ctx *c, PlaneScale &p, int sw, int sh, int dw, int dh,
           mfb[(size_t)l * 8 + (j >> 2)] |= (int32_t)(hi << (8 * (j & 3)));
           mfb[(size_t)l * 8 + 4 + (j >> 2)] |= (int32_t)(lo << (8 * (j & 3)));
         }
+      // The matrix-core v-pass (scale.hip) for the interior tile rows of those columns when they
+      // all share one v filter at a 2-row step: A[m][k] = tap k - 2m - delta of it (0 outside the
+      // 8 taps), delta = the parity of its first row (the window starts at the even row below),
+      // split as tap = 128 fh + fl: fragments fh, fl and 2 fl, lane l holding A[l & 15][16 (l >> 4)
+      // + j] in byte j (the h-pass's k map)
+      const int gyt = (dh + th - 1) / th, ya = th, yb = th * (gyt - 1);
+      bool vok = gyt >= 3 && vt == 8 && 2 * 64 * kPlaneStride + 16 <= (int)p.lds;
+      for (int y = ya; y < yb && vok; y++) {
+        vok = p.vf.pos[y] == p.vf.pos[ya] + 2 * (y - ya);
+        for (int k = 0; k < vt && vok; k++) vok = p.vf.coeff[(size_t)y * vt + k] == p.vf.coeff[(size_t)ya * vt + k];
+      }
+      int fsum = 0;
+      for (int k = 0; k < vt && vok; k++) {
+        const int cv = p.vf.coeff[(size_t)ya * vt + k], fl = ((cv + 64) & 127) - 64;
+        vok = (cv - fl) / 128 >= -128 && (cv - fl) / 128 <= 127;
+        fsum += cv;
+      }
+      g.mv_by0 = g.mv_by1 = 0;
+      g.mv_k = 0;
+      if (vok) {
+        const int delta = p.vf.pos[ya] & 1;
+        for (int l = 0; l < 64; l++)
+          for (int j = 0; j < 16; j++) {
+            const int m = l & 15, k = 16 * (l >> 4) + j, t = k - 2 * m - delta;
+            const int cv = (t >= 0 && t < 8) ? p.vf.coeff[(size_t)ya * vt + t] : 0;
+            const int fl = ((cv + 64) & 127) - 64, fh = (cv - fl) / 128;
+            const int vals[3] = {fh, fl, 2 * fl};
+            for (int f = 0; f < 3; f++)
+              mfb[kMvFragOff + (size_t)(f * 64 + l) * 4 + (j >> 2)] |= (int32_t)((uint32_t)(uint8_t)(int8_t)vals[f] << (8 * (j & 3)));
+          }
+        g.mv_by0 = 1;
+        g.mv_by1 = gyt - 1;
+        g.mv_k = 128 * fsum + (64 << 12);
+      }
       if ((rc = dmalloc(&p.mfb, mfb.size()))) return rc;
       HIP_TRY(hipMemcpy(p.mfb, mfb.data(), mfb.size() * 4, hipMemcpyHostToDevice));
       g.mf_bx0 = 1;

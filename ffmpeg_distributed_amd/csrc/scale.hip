@@ -65,7 +65,14 @@ struct ScaleGeom {
   uint32_t gx_magic, gxy_magic;  // 0 when the divisor is 1
   int mf_bx0, mf_bx1, mf_hs;     // tile columns [mf_bx0, mf_bx1) take the matrix-core h-pass
                                  // (one filter, hsum mf_hs; the host checks: api.hip)
+  int mv_by0, mv_by1, mv_k;      // of those, tile rows [mv_by0, mv_by1) take the matrix-core v-pass
+                                 // (one filter; mv_k = 128 * its tap sum + (64 << 12))
 };
+
+// The matrix-core v-pass's byte planes (k_scale): per output column, the h values of the tile's
+// window rows as hi bytes ([col][row], this stride) and then as lo bytes ^ 0x80
+constexpr int kPlaneStride = 144;  // >= the 136 window rows of a 64-row 2:1 tile, 16-byte multiple
+constexpr int kMvFragOff = 512;    // words of mfb before the v-pass A fragments (3 x 64 lanes x 16 B)
 
 // t / d for 0 <= t < 2^31: with m = ceil(2^32 / d), umulhi(t, m) is t / d or one more (the
 // error t (m - 2^32/d) / 2^32 < 1), corrected by one compare; d = 1: m = 0
@@ -228,6 +235,69 @@ __global__ __launch_bounds__(64 * scale_waves(TH)) void k_scale(const SegList sr
       }
     }
     __syncthreads();  // every wave's window reads done: the pairs go over the rows
+    if (by >= g.mv_by0 && by < g.mv_by1) {
+      // The v-pass on the matrix cores as well (interior tile rows: one v filter, pos[y] = 2y + c).
+      // With h = 256 hi + lo (hi: the int16's high byte as int8; lo its low byte, stored as
+      // lo ^ 0x80 = lo - 128) and each tap f = 128 fh + fl (fl in [-64, 64)):
+      //   sum h f = 32768 S1 + 128 X + S4 + 128 F,  S1 = sum hi fh,  X = sum hi (2 fl) + sum lo' fh,
+      //   S4 = sum lo' fl  (F = the tap sum),
+      // four v_mfma_i32_16x16x64_i8 per 16 x 16 block of outputs, every product exact in i32:
+      // A = 64 plane bytes (window rows 32 rb ..) of 16 columns, B = the filter's band (host-built:
+      // output row n of the block reads window rows 2n + delta + j), so D's lane (n, g4) holds
+      // output row n, columns 4 g4 .. 4 g4 + 3 of the block.  Each wave writes the planes of the
+      // columns it computed in the h-pass, then (after a barrier) takes row block rb = wave.
+      uint8_t *phi = (uint8_t *)smem, *plo = phi + 64 * kPlaneStride;
+      const int colw = 16 * wave + n;
+#pragma unroll
+      for (int m = 0; m < kMfBlocks; m++) {
+        if (16 * m < nrows) {  // (rows past nrows repeat the last one: finite, met by zero taps)
+          const uint32_t hw = __builtin_amdgcn_perm(pk[m][1], pk[m][0], 0x07050301u);
+          const uint32_t lw = __builtin_amdgcn_perm(pk[m][1], pk[m][0], 0x06040200u) ^ 0x80808080u;
+          *(uint32_t *)(phi + colw * kPlaneStride + 16 * m + 4 * g4) = hw;
+          *(uint32_t *)(plo + colw * kPlaneStride + 16 * m + 4 * g4) = lw;
+        }
+      }
+      const u32x4 *mva = (const u32x4 *)(mfb + kMvFragOff);
+      const v4i bfh = __builtin_bit_cast(v4i, mva[lane]), bfl = __builtin_bit_cast(v4i, mva[64 + lane]),
+                b2fl = __builtin_bit_cast(v4i, mva[128 + lane]);
+      const v4i z = {0, 0, 0, 0}, kv = {g.mv_k, g.mv_k, g.mv_k, g.mv_k};
+      __syncthreads();  // every column's planes written
+      uint32_t W[4];  // W[cb]: output row n, columns 16 cb + 4 g4 .. + 3 (bytes)
+#pragma unroll
+      for (int cb = 0; cb < 4; cb++) {
+        // rows 32 wave .. 32 wave + 63 of column 16 cb + n (the last block's reads run past the
+        // column into the next one: bytes met by zero taps)
+        const int off = (16 * cb + n) * kPlaneStride + 32 * wave + 16 * g4;
+        const v4i ah = __builtin_bit_cast(v4i, *(const u32x4 *)(phi + off));
+        const v4i al = __builtin_bit_cast(v4i, *(const u32x4 *)(plo + off));
+        const v4i s1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bfh, z, 0, 0, 0);
+        v4i x = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, b2fl, z, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bfh, x, 0, 0, 0);
+        const v4i s4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bfl, kv, 0, 0, 0);
+        uint32_t v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = (uint32_t)min(max(((s1[i] << 15) + (x[i] << 7) + s4[i]) >> 19, 0), 255);
+        W[cb] = __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0400u) | __builtin_amdgcn_perm(v[3], v[2], 0x04000c0cu);
+      }
+      // 4 x 4 transpose of (cb, g4) across lanes n, n + 16, n + 32, n + 48: then lane (n, g4)
+      // holds columns 16 g4 .. 16 g4 + 15 of row n, one 16-byte store (a wave: 16 full rows)
+      auto swap32 = [](uint32_t &a_, uint32_t &b_) {
+        const auto r = __builtin_amdgcn_permlane32_swap(a_, b_, false, false);
+        a_ = r[0];
+        b_ = r[1];
+      };
+      auto swap16 = [](uint32_t &a_, uint32_t &b_) {
+        const auto r = __builtin_amdgcn_permlane16_swap(a_, b_, false, false);
+        a_ = r[0];
+        b_ = r[1];
+      };
+      swap32(W[0], W[2]);
+      swap32(W[1], W[3]);
+      swap16(W[0], W[1]);
+      swap16(W[2], W[3]);
+      *(u32x4 *)(d + (size_t)(y0 + 16 * wave + n) * g.d_stride + x0 + 16 * g4) = u32x4{W[0], W[1], W[2], W[3]};
+      return;
+    }
 #pragma unroll
     for (int m = 0; m < kMfBlocks; m++) {
       const int pa = 8 * m + 2 * g4;  // the pairs of D rows 4 g4 .. 4 g4 + 3 of block m

@@ -146,6 +146,53 @@ def test_scale_2to1_matrix_core_hpass(kind, full):
         assert got[i] == ref[i], (i, len(got[i]), len(ref[i]), first_diff(got[i], ref[i]))
 
 
+def _extreme_2to1_frame(w, h, seed, full):
+    """Pixels that drive both passes of a 2:1 bicubic to their extremes: horizontal bands of
+    0 / 255 rows (the v filter's negative lobes against the largest h values, 32767 after the
+    clamp, and the smallest), vertical full-swing stripes, a pixel checker and noise, each in a
+    region several 64-row tiles tall; tv range input keeps 0..255 (swscale clamps it)."""
+    rng = np.random.default_rng(seed)
+    y = np.zeros((h, w), np.uint8)
+    q = w // 4
+    rows = np.arange(h)[:, None]
+    cols = np.arange(q)[None, :]
+    y[:, :q] = np.where((rows // (1 + seed % 3)) % 2 + 0 * cols, 255, 0)  # horizontal bands
+    y[:, q:2 * q] = np.where((cols // 2) % 2 + 0 * rows, 255, 0)          # vertical stripes
+    y[:, 2 * q:3 * q] = np.where((rows + cols) % 2, 255, 0)               # pixel checker
+    y[:, 3 * q:] = rng.integers(0, 256, (h, w - 3 * q))                   # noise
+    y[h // 3: h // 3 + 70, :] = 255                                  # a white band across
+    y[2 * h // 3: 2 * h // 3 + 5, :] = 0
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    u = np.where((np.arange(ch)[:, None] // 3) % 2, 255, 0).astype(np.uint8).repeat(cw, 1)
+    v = rng.integers(0, 256, (ch, cw)).astype(np.uint8)
+    v[:, : cw // 2] = np.where((np.arange(cw // 2)[None, :] + np.arange(ch)[:, None]) % 2, 0, 255)
+    return pack_i420(y, u, v)
+
+
+@pytest.mark.parametrize("full", [False, True])
+def test_scale_2to1_matrix_core_vpass(full):
+    """Exact 2:1 downscales also take k_scale's matrix-core v-pass on their interior tiles (tile
+    rows but the first and last, h values split into signed hi / offset lo bytes, taps into
+    128 fh + fl): content at both passes' extremes, tv and pc range; the scaled planes equal the
+    oracle's swscale restatement and the JPEGs its encoder, byte for byte."""
+    w, h, n = 1536, 896, 2
+    frames = np.stack([_extreme_2to1_frame(w, h, s, full) for s in range(n)])
+    with MjpegEncoder(0, w, h, w // 2, h // 2, qscale=4, full_range=full, max_batch=n) as enc:
+        enc.submit(frames)
+        enc.sync()
+        planes = [enc.debug_planes(i) for i in range(n)]
+        got = enc.fetch()
+    for i in range(n):
+        y, u, v = split_i420(frames[i], w, h)
+        gy, gu, gv = split_i420(planes[i], w // 2, h // 2)
+        ry = oracle.scale_plane(y, w // 2, h // 2, 0 if full else 1)
+        assert (gy == ry).all(), (i, np.argwhere(gy != ry)[:5])
+        for g, p in ((gu, u), (gv, v)):
+            r = oracle.scale_plane(p, w // 4, h // 4, 0 if full else 2, chroma=True)
+            assert (g == r).all(), (i, np.argwhere(g != r)[:5])
+    assert got == oracle_frames(frames, w, h, 4, full, w // 2, h // 2)
+
+
 def test_huffman_optimal_scaled_batches():
     """optimal tables with -vf scale, ragged batches and a reused context."""
     sw, sh, dw, dh, q = 160, 96, 80, 48, 3
