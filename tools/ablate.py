@@ -31,7 +31,7 @@ CSRC = os.path.join(ROOT, "ffmpeg_distributed_amd", "csrc")
 
 EMIT = ("      emit_block(s_pk + lane, mask, diff, s_zd, s_m2, q);\n"
         "      q.finish();\n")
-WIDE = "    const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);\n    if (cur_active && !((wide >> lane) & 1ull)) {\n      emit_block"
+WIDE = "    const uint64_t wide = wave_parallel_blocks(cur_active ? __popcll(mask) : 0);\n    if (cur_active && !((wide >> lane) & 1ull)) {\n"
 EXACT = "  const uint32_t *col = (const uint32_t *)((const uint8_t *)pkcol + d.w);\n"
 SCREEN = "      column_screen(s_pk, lane, s_skip, s_thr, dc, mlo, mhi, skip_st, (t & 3) == 0);"
 ROWPASS = "    row_pass<RC>(raw, tab, s_rc, s_pk, lane);"
@@ -63,7 +63,7 @@ SUBS = {
     "nohbm": [(FBASE, "  auto frame_base = [&](int f) { return seg_frame(frames, f & 1, g.frame_stride); };")],
     "noemit": [(EMIT, "      q.emit(((uint32_t)__popcll(mask) << 8) ^ ((uint32_t)diff & 255u), 16);\n"
                       "      q.finish();\n"),
-               (WIDE, "    const uint64_t wide = 0;\n    if (cur_active && !((wide >> lane) & 1ull)) {\n      emit_block")],
+               (WIDE, "    const uint64_t wide = 0;\n    if (cur_active && !((wide >> lane) & 1ull)) {\n")],
     "noexact": [(EXACT, "  if (d.x != 0u) return 1 + (int)(d.y & 1u);\n" + EXACT)],
     "noscreen": [(SCREEN, "      dc = (int)(s_pk[lane] & 255u) - 128;")],
     "nodct": [(ROWPASS, "    {\n#pragma unroll\n      for (int r = 0; r < 8; r++) {\n"
