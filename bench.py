@@ -26,6 +26,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -497,9 +498,26 @@ def rooflines(kt, fpl, mean_jpeg, pmc, optimal, scaled, step_ms=None, seg=None):
     return primary, out
 
 
+def torchrun_argv(gpus: int, argv, port: int):
+    """`--gpus N` (N > 1) outside a launcher: the driver's own launch line, one rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
 def main():
     global W, H, DW, DH, Q, SEG, FULL, HUFF, WTEXT
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not (a.cpu_baseline_only or a.e2e_only):
+        # started without a launcher: run the ranks as a child (before anything touches the GPU)
+        # and exit with its code, so `python bench.py --gpus N` measures N GPUs, not one
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        sys.exit(subprocess.run(torchrun_argv(a.gpus, sys.argv[1:], port)).returncode)
+    if "WORLD_SIZE" in os.environ and a.gpus != int(os.environ["WORLD_SIZE"]):
+        print(f"bench.py: --gpus {a.gpus} under a launcher of {os.environ['WORLD_SIZE']} ranks: "
+              "measuring the launcher's ranks", file=sys.stderr)
     W, H, DW, DH, Q, SEG, FULL, HUFF, WTEXT = WORKLOADS[a.workload]
     if a.huffman:
         HUFF = a.huffman

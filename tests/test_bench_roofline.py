@@ -68,3 +68,14 @@ def test_no_pmc_gives_null_traffic(workload):
     primary, ents = bench.rooflines({"encode": 1.0, "scale": 0.0, "huff": 0.0}, 240, 3e5, {}, False, False,
                                     step_ms=0.6, seg=120)
     assert primary["traffic"] is None and ents[0]["traffic"] is None
+
+
+def test_gpus_without_launcher_runs_the_driver_launch_line():
+    """`python bench.py --gpus N` outside torchrun re-runs itself under the driver's launch line
+    (one rank per GPU, rendezvous on 127.0.0.1) as a child, with the same arguments."""
+    argv = bench.torchrun_argv(4, ["--gpus", "4", "--steps", "5"], 29511)
+    assert argv[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in argv and "--nnodes=1" in argv
+    assert argv[argv.index("--master-addr") + 1] == "127.0.0.1"
+    assert argv[argv.index("--master-port") + 1] == "29511"
+    assert argv[-5].endswith("bench.py") and argv[-4:] == ["--gpus", "4", "--steps", "5"]
